@@ -1,0 +1,116 @@
+/*
+ * include/nmfc.h -- batched MI355X restart-sweep engine (additive C ABI of nmfconsensus_amd/libnmf.so).
+ *
+ * One call replaces the reference's restart fan-out and consensus reduction:
+ *   createJobArray / runNMFinJobs   nmf.r:53-70, 106-113  (k x restart job grid, per-job seeds)
+ *   doNMF                           nmf.r:23-51           (per-job init + .C("nmf_mu"))
+ *   nmf_mu loop + stop rule         libnmf/nmf_mu.c:167-293
+ *   computeConsensusMatrixFromClusterings  nmf.r:121-144 (labels, connectivity counts, /R)
+ *   cophenetic correlation          nmf.r:165-172         (nmfc_cophenetic)
+ * Plain pointers and sizes only.  All matrices are column-major fp64 like libnmf.
+ */
+#ifndef NMFC_H
+#define NMFC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Stop rules (DESIGN.md "Stop rules"). */
+enum {
+  NMFC_STOP_FIXED = 0,          /* run exactly maxiter iterations */
+  NMFC_STOP_REF_COMPAT = 1,     /* nmf_mu.c:253-282 as the reference executes it (zero-padded h0) */
+  NMFC_STOP_ARGMAX_STABLE = 2   /* same counter, per-sample argmax class (the check's intent) */
+};
+
+/* Label rules for the consensus (nmf.r:128). */
+enum {
+  NMFC_LABEL_ARGMAX = 0,        /* row of the column maximum (nmf.r:127 comment, BROAD intent) */
+  NMFC_LABEL_R_ORDER = 1        /* apply(H,2,order)[1,] as written at nmf.r:128: the column minimum */
+};
+
+typedef struct nmfc_sweep_opts {
+  int maxiter;        /* nmf.r maxniter (cap; default 10000) */
+  int stop_rule;      /* NMFC_STOP_* */
+  int label_rule;     /* NMFC_LABEL_* */
+  uint32_t seed;      /* registry seed: job seed = seed + job_id - 1 (job_id 1-based, expand.grid order) */
+  int min_init;       /* generateMatrix range (options_t.min_init / max_init, default 0 / 1) */
+  int max_init;
+  int job_begin;      /* shard [job_begin, job_end) of the 0-based job list; job_end < 0 => all jobs */
+  int job_end;
+  int check_every;    /* host polls the stopped-restart count every this many iterations (default 16) */
+  int verbose;        /* 0 quiet; 1 per-sweep summary on stderr */
+} nmfc_sweep_opts;
+
+/* Outputs.  Every pointer may be NULL.  Host memory unless *_on_device is set.
+ * Jobs are indexed 0..njobs-1 in expand.grid order (k fastest): job j has k = ks[j % nk] and restart
+ * r = j / nk + 1; per-job arrays are indexed by (j - job_begin). */
+typedef struct nmfc_result {
+  int32_t* counts;          /* nk x n x n integer connectivity counts of this shard's jobs */
+  int counts_on_device;     /* counts is a device pointer (e.g. a torch tensor for an RCCL all-reduce) */
+  double* consensus;        /* nk x n x n  counts / R  (only meaningful for a full, unsharded run) */
+  int32_t* labels;          /* njobs_shard x n, 1-based */
+  int32_t* iters;           /* njobs_shard: iterations run */
+  int32_t* stopped_early;   /* njobs_shard: 1 if the stop rule fired (nmf_mu.c:270 writes *maxiter), else 0 */
+  double* W;                /* sum over shard jobs of m*k, job-major, each m x k column-major */
+  double* H;                /* sum over shard jobs of k*n, job-major, each k x n column-major */
+  /* filled by the engine: */
+  double seconds_total;     /* wall time of the run inside the engine */
+  double seconds_iterate;   /* part spent in the iteration loop */
+  long long restart_iterations; /* sum of iterations over the shard's restarts */
+  int max_iter_run;         /* largest iteration count */
+} nmfc_result;
+
+typedef struct nmfc_engine nmfc_engine;
+
+/* Creates an engine on HIP device `device` (-1: current device) with data matrix A (m x n, ld m).
+ * a_on_device != 0: A is a device pointer (copied device-to-device into the engine's layouts). */
+nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a_on_device);
+void nmfc_engine_destroy(nmfc_engine* e);
+
+void nmfc_default_opts(nmfc_sweep_opts* o);
+
+/* Runs the k-sweep: for every job of the shard, init (generateMatrix(ran) stream with the job seed,
+ * or the caller's W_init/H_init when given), MU iterations under the stop rule, labels, counts.
+ * W_init / H_init (optional): job-major initial factors for the shard, layouts as in nmfc_result.
+ * Returns 0 on success; nonzero with nmfc_last_error() set otherwise. */
+int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_sweep_opts* opts,
+                    const double* W_init, const double* H_init, nmfc_result* out);
+
+/* Convenience: create, run, destroy. */
+int nmfc_sweep(const double* A, int m, int n, const int* ks, int nk, int R, const nmfc_sweep_opts* opts,
+               nmfc_result* out);
+
+/* computeConsensusMatrixFromClusterings (nmf.r:121-144) on the GPU for R results of one rank k:
+ * Hs holds R consecutive k x n column-major H matrices (host).  labels (R x n, 1-based), counts (n x n
+ * int) and consensus (n x n, counts / R) are host outputs; each may be NULL. */
+int nmfc_consensus(const double* Hs, int k, int n, int R, int label_rule, int32_t* labels, int32_t* counts,
+                   double* consensus);
+
+/* Cophenetic correlation of one consensus matrix (nmf.r:165-172): average-linkage hclust on
+ * d = 1 - C, cophenetic distances, Pearson correlation over the n(n-1)/2 pairs (unrounded; R
+ * applies signif(., 4) afterwards).  order_out (n, 1-based, may be NULL) receives the dendrogram
+ * leaf order (HC$order); merge_out (2*(n-1), may be NULL) R-style merge matrix; height_out (n-1). */
+double nmfc_cophenetic(const double* C, int n, int32_t* order_out, int32_t* merge_out, double* height_out);
+
+/* cutree(HC, k) membership (nmf.r:177) from a merge matrix produced by nmfc_cophenetic. 1-based. */
+int nmfc_cutree(const int32_t* merge, int n, int k, int32_t* membership_out);
+
+/* Diagnostics. */
+const char* nmfc_last_error(void);
+const char* nmfc_version(void);
+/* Per-kernel device time (ms) accumulated over the last run, measured with HIP events on the
+ * engine's stream: kernel ids 0 = wta (W^T[A|W] MFMA), 1 = hupdate, 2 = ahtw (A H^T MFMA + W update),
+ * 3 = init, 4 = labels+counts.  Returns the number of launches of that kernel. */
+long long nmfc_engine_kernel_time(nmfc_engine* e, int kernel_id, double* ms_out);
+/* Enables per-launch event timing (adds small overhead; used by bench.py's roofline leg). */
+void nmfc_engine_set_timing(nmfc_engine* e, int enable);
+/* Algorithmic flop per launch of the dominant kernel in the last run, for the roofline report. */
+double nmfc_engine_kernel_flops(nmfc_engine* e, int kernel_id);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

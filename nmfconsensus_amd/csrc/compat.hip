@@ -1,0 +1,211 @@
+// compat.hip -- the libnmf entry points of include/libnmf_compat.h, MI355X-native.
+// nmf_mu's loop runs on the batched engine (engine.hip) with a batch of one restart; calculateNorm /
+// calculateMaxchange are GPU reductions; the option helpers and the rand()-based init stay host C,
+// exactly as the reference's (they share libc's global rand() state with the caller).
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <ctime>
+#include <vector>
+
+#include "../../include/libnmf_compat.h"
+#include "../../include/nmfc.h"
+#include "nmfc_kernels.hpp"
+
+extern "C" {
+
+// setdefaultopts.c:38-52
+void set_default_opts(options_t* opts) {
+  opts->rep = 1;
+  opts->init = ran;
+  opts->min_init = 0;
+  opts->max_init = 1;
+  opts->w_out = "final_w.matrix";
+  opts->h_out = "final_h.matrix";
+  opts->TolX = 1.0E-04;
+  opts->TolFun = 1.0E-04;
+  opts->nndsvd_maxiter = -1;
+  opts->nndsvd_blocksize = 64;
+  opts->nndsvd_tol = 2E-16;
+  opts->nndsvd_ncv = -1;
+}
+
+// checkarguments.c:50-78 -- same predicate, same errno and message
+int checkArguments(const char* a, const int k, int iter, const char* w0, const char* h0, options_t* opts) {
+  if (!a || k < 0 || iter < 0 || (w0 && w0[0] == '\0') || (h0 && h0[0] == '\0') || opts->rep < 0 ||
+      opts->min_init < 0 || !opts->w_out || !opts->h_out || opts->TolX < 0 || opts->TolFun < 0) {
+    errno = EDOM;
+    perror("Error in arguments passed to nmfDriver.");
+    return 1;
+  }
+  return 0;
+}
+
+// checkmatrices.c:43-81
+int checkMatrices(const double* a, const double* w, const double* h, const int m, const int n, const int k) {
+  long i;
+  for (i = 0; i < (long)m * n && a[i] >= 0.; i++) {
+  }
+  if (i < (long)m * n) {
+    printf("negative element in a[%ld]\n", i);
+    return 1;
+  }
+  for (i = 0; i < (long)m * k && w[i] >= 0.; i++) {
+  }
+  if (i < (long)m * k) {
+    printf("negative element in w[%ld] = %f\n", i, w[i]);
+    return 1;
+  }
+  for (i = 0; i < (long)k * n && h[i] >= 0.; i++) {
+  }
+  if (i < (long)k * n) {
+    printf("negative element in h[%ld]\n", i);
+    return 1;
+  }
+  return 0;
+}
+
+// randnumber.c:27-35 -- libc rand(), time-seeded on first use like the reference
+double randnumber(const int min, const int max) {
+  static int initialised = 0;
+  if (!initialised) {
+    srand((unsigned)time(NULL));
+    initialised = 1;
+  }
+  const int prod = (int)((unsigned)(max - min) * (unsigned)rand());
+  return (double)min + ((double)prod / (double)(RAND_MAX));
+}
+
+// generatematrix.c:96-137 (ran); nndsvd (generatematrix.c:138-294) is out of scope -> ENOSYS
+void generateMatrix(const int* pm, const int* pn, const int* pk, init_t* pinit, const int* pmin, const int* pmax,
+                    double* matrixW, double* matrixH, double* matrixA, options_t* opts) {
+  (void)matrixA;
+  (void)opts;
+  const int m = *pm, n = *pn, k = *pk;
+  if (!matrixW || !matrixH) {
+    // the reference mallocs a buffer the caller never sees (generatematrix.c:118-121)
+    errno = EINVAL;
+    perror("generateMatrix: W and H buffers must be provided");
+    return;
+  }
+  if (*pinit == ran) {
+    for (long i = 0; i < (long)m * k; ++i) matrixW[i] = randnumber(*pmin, *pmax);
+    for (long i = 0; i < (long)k * n; ++i) matrixH[i] = randnumber(*pmin, *pmax);
+  } else {
+    errno = ENOSYS;
+    perror("generateMatrix: nndsvd initialisation is not provided by this engine");
+  }
+}
+
+// nmf_mu.c:84-315 on the GPU engine
+double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int* maxiter, const double* pTolX,
+              const double* pTolFun) {
+  (void)pTolX;
+  (void)pTolFun;   // read but unused, as in the reference (nmf_mu.c:92-93)
+  const int m = *pm, n = *pn, k = *pk;
+  if (*maxiter < 1) {
+    printf("Exiting nmf_mu after %i\n", 1);
+    return 0;
+  }
+  nmfc_engine* e = nmfc_engine_create(-1, a, m, n, 0);
+  if (!e) {
+    fprintf(stderr, "Error in nmf_mu: %s\n", nmfc_last_error());
+    return -1;
+  }
+  nmfc_sweep_opts o;
+  nmfc_default_opts(&o);
+  o.maxiter = *maxiter;
+  o.stop_rule = NMFC_STOP_REF_COMPAT;
+  o.check_every = 64;
+  int32_t iters = 0, early = 0;
+  nmfc_result r = {};
+  r.iters = &iters;
+  r.stopped_early = &early;
+  r.W = w0;
+  r.H = h0;
+  const int ks[1] = {k};
+  int rc = nmfc_engine_run(e, ks, 1, 1, &o, w0, h0, &r);
+  nmfc_engine_destroy(e);
+  if (rc != 0) {
+    fprintf(stderr, "Error in nmf_mu: %s\n", nmfc_last_error());
+    return -1;
+  }
+  // nmf_mu.c:270 writes *maxiter only on the early exit; :296 prints the loop counter (cap + 1 when
+  // the loop ran to the cap).
+  int printed = iters;
+  if (early)
+    *maxiter = iters;
+  else
+    printed = iters + 1;
+  printf("Exiting nmf_mu after %i\n", printed);
+  return 0;
+}
+
+// calculatenorm.c:44-78 -- d = a - w h and ||d||_F / sqrt(m n), one fused GPU pass + host sum of
+// per-block partials in block order (deterministic).
+double calculateNorm(double* a, double* w, double* h, double* d, int m, int n, int k) {
+  const size_t la = (size_t)m * n, lw = (size_t)m * k, lh = (size_t)k * n;
+  double *da = nullptr, *dw = nullptr, *dh = nullptr, *dd = nullptr, *dp = nullptr;
+  const int blocks = (int)std::min<size_t>((la + nmfc::NT - 1) / nmfc::NT, 1024);
+  std::vector<double> part(blocks);
+  double result = NAN;
+  if (hipMalloc(&da, la * 8) || hipMalloc(&dw, lw * 8) || hipMalloc(&dh, lh * 8) || hipMalloc(&dd, la * 8) ||
+      hipMalloc(&dp, blocks * 8))
+    goto done;
+  if (hipMemcpy(da, a, la * 8, hipMemcpyHostToDevice) || hipMemcpy(dw, w, lw * 8, hipMemcpyHostToDevice) ||
+      hipMemcpy(dh, h, lh * 8, hipMemcpyHostToDevice))
+    goto done;
+  hipLaunchKernelGGL(nmfc::k_norm_partial, dim3(blocks), dim3(nmfc::NT), 0, 0, da, dw, dh, dd, m, n, k, dp);
+  if (hipGetLastError() != hipSuccess) goto done;
+  if (hipMemcpy(d, dd, la * 8, hipMemcpyDeviceToHost) || hipMemcpy(part.data(), dp, blocks * 8, hipMemcpyDeviceToHost))
+    goto done;
+  {
+    double ss = 0.0;
+    for (int b = 0; b < blocks; ++b) ss += part[b];
+    result = sqrt(ss) / sqrt((double)m * n);
+  }
+done:
+  if (std::isnan(result)) fprintf(stderr, "calculateNorm: device failure\n");
+  (void)hipFree(da);
+  (void)hipFree(dw);
+  (void)hipFree(dh);
+  (void)hipFree(dd);
+  (void)hipFree(dp);
+  return result;
+}
+
+// calculatemaxchange.c:42-71 -- max|mat0 - mat| / (sqrteps + max|mat0|); mat0 -= mat (exact, order-free)
+double calculateMaxchange(double* mat, double* mat0, int m, int n, const double sqrteps) {
+  const size_t len = (size_t)m * n;
+  double *dm = nullptr, *dm0 = nullptr, *dp = nullptr;
+  const int blocks = (int)std::min<size_t>((len + nmfc::NT - 1) / nmfc::NT, 1024);
+  std::vector<double> part(2 * blocks);
+  double result = NAN;
+  if (hipMalloc(&dm, len * 8) || hipMalloc(&dm0, len * 8) || hipMalloc(&dp, 2 * blocks * 8)) goto done;
+  if (hipMemcpy(dm, mat, len * 8, hipMemcpyHostToDevice) || hipMemcpy(dm0, mat0, len * 8, hipMemcpyHostToDevice))
+    goto done;
+  hipLaunchKernelGGL(nmfc::k_maxchange_partial, dim3(blocks), dim3(nmfc::NT), 0, 0, dm, dm0, (long)len, dp);
+  if (hipGetLastError() != hipSuccess) goto done;
+  if (hipMemcpy(mat0, dm0, len * 8, hipMemcpyDeviceToHost) ||
+      hipMemcpy(part.data(), dp, 2 * blocks * 8, hipMemcpyDeviceToHost))
+    goto done;
+  {
+    double mx0 = 0.0, mxd = 0.0;
+    for (int b = 0; b < blocks; ++b) {
+      mx0 = fmax(mx0, part[2 * b]);
+      mxd = fmax(mxd, part[2 * b + 1]);
+    }
+    result = mxd / (sqrteps + mx0);
+  }
+done:
+  if (std::isnan(result)) fprintf(stderr, "calculateMaxchange: device failure\n");
+  (void)hipFree(dm);
+  (void)hipFree(dm0);
+  (void)hipFree(dp);
+  return result;
+}
+
+}  // extern "C"

@@ -1,0 +1,688 @@
+// engine.hip -- host side of the batched MU restart engine (C ABI in include/nmfc.h).
+//
+// Replaces the reference's restart driver (nmf.r:53-70, 106-113), its per-job nmf_mu loop
+// (libnmf/nmf_mu.c:167-293) and the consensus reduction (nmf.r:121-144) with one batched sweep on
+// one MI355X: all (k, restart) jobs of a shard are packed into 64-column panels of a stacked W/H,
+// and every MU iteration is three launches on one HIP stream:
+//   k_wta     G = W^T A and the panel Grams W^T W            (fp64 MFMA, split over fixed gene chunks)
+//   k_hupdate H update, H H^T, stability check per restart   (one workgroup per restart)
+//   k_ahtw    A H^T fused with W0 (H H^T) and the W update   (fp64 MFMA, epilogue in LDS)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/nmfc.h"
+#include "nmfc_kernels.hpp"
+
+using namespace nmfc;
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+#define HCHECK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) {                                                                 \
+      set_err("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return -1;                                                                            \
+    }                                                                                       \
+  } while (0)
+
+long round_up(long v, long a) { return (v + a - 1) / a * a; }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (need == 0) return 0;
+    hipError_t e = hipMalloc(&p, need);
+    if (e != hipSuccess) {
+      set_err("hipMalloc(%zu) failed: %s", need, hipGetErrorString(e));
+      p = nullptr;
+      return -1;
+    }
+    bytes = need;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+// 31x31 jump matrices J[c] = M^(c*RCHUNK) mod 2^32 of the recurrence r[i] = r[i-31] + r[i-3]
+// acting on the ordered window (r[i-31], ..., r[i-1]).
+void mat_mul31(const uint32_t* A, const uint32_t* B, uint32_t* C) {
+  for (int i = 0; i < 31; ++i)
+    for (int j = 0; j < 31; ++j) {
+      uint32_t s = 0;
+      for (int q = 0; q < 31; ++q) s += A[i * 31 + q] * B[q * 31 + j];
+      C[i * 31 + j] = s;
+    }
+}
+
+std::vector<uint32_t> make_jump_table(int nchunks) {
+  std::vector<uint32_t> M(31 * 31, 0), P(31 * 31, 0), T(31 * 31), R(31 * 31);
+  for (int q = 0; q < 30; ++q) M[q * 31 + q + 1] = 1;
+  M[30 * 31 + 0] = 1;   // r[i-31]
+  M[30 * 31 + 28] += 1; // r[i-3]
+  // P = M^RCHUNK by repeated squaring
+  for (int i = 0; i < 31; ++i) P[i * 31 + i] = 1;
+  std::vector<uint32_t> base = M;
+  for (int e = RCHUNK; e > 0; e >>= 1) {
+    if (e & 1) {
+      mat_mul31(P.data(), base.data(), T.data());
+      P = T;
+    }
+    mat_mul31(base.data(), base.data(), T.data());
+    base = T;
+  }
+  std::vector<uint32_t> table((size_t)std::max(nchunks, 1) * 961, 0);
+  for (int i = 0; i < 31; ++i) table[i * 31 + i] = 1;
+  for (int c = 1; c < nchunks; ++c) {
+    mat_mul31(P.data(), &table[(size_t)(c - 1) * 961], &table[(size_t)c * 961]);
+  }
+  return table;
+}
+
+enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_LABEL = 4, KID_N = 5 };
+
+}  // namespace
+
+struct nmfc_engine {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  int m = 0, n = 0;
+  long m_pad = 0, n_pad = 0, n_cols_pad = 0;
+  int kchunk = 0, nsplit = 0;
+  DevBuf Acm, Arm;
+  // per-run buffers (grow-only)
+  DevBuf W, H, Gpart, SWpart, SHp;
+  DevBuf rinfo, stop_iter, stop_reason, unchanged, classes, n_stopped;
+  DevBuf prb, pre, pcs, pck, pcr;
+  DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp;
+  int jump_chunks = 0;
+  int* h_stopped = nullptr;   // pinned, 2 slots
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  struct Pending {
+    int kid;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  double kms[KID_N] = {0};
+  long long kcount[KID_N] = {0};
+  double kflops[KID_N] = {0};
+};
+
+namespace {
+
+hipEvent_t take_event(nmfc_engine* e) {
+  if (!e->ev_pool.empty()) {
+    hipEvent_t ev = e->ev_pool.back();
+    e->ev_pool.pop_back();
+    return ev;
+  }
+  hipEvent_t ev;
+  if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+  return ev;
+}
+
+void drain_timing(nmfc_engine* e) {
+  for (auto& pnd : e->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(pnd.b) == hipSuccess && hipEventElapsedTime(&ms, pnd.a, pnd.b) == hipSuccess) {
+      e->kms[pnd.kid] += ms;
+      e->kcount[pnd.kid] += 1;
+    }
+    e->ev_pool.push_back(pnd.a);
+    e->ev_pool.push_back(pnd.b);
+  }
+  e->pending.clear();
+}
+
+struct TimedLaunch {
+  nmfc_engine* e;
+  int kid;
+  hipEvent_t a = nullptr;
+  TimedLaunch(nmfc_engine* e_, int kid_) : e(e_), kid(kid_) {
+    if (e->timing) {
+      a = take_event(e);
+      if (a) (void)hipEventRecord(a, e->st);
+    }
+  }
+  ~TimedLaunch() {
+    if (e->timing && a) {
+      hipEvent_t b = take_event(e);
+      if (b) {
+        (void)hipEventRecord(b, e->st);
+        e->pending.push_back({kid, a, b});
+      }
+    } else if (!e->timing) {
+      e->kcount[kid] += 1;
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* nmfc_last_error(void) { return g_err.c_str(); }
+const char* nmfc_version(void) { return "nmfconsensus_amd 0.1 (gfx950, fp64 MFMA)"; }
+
+void nmfc_default_opts(nmfc_sweep_opts* o) {
+  memset(o, 0, sizeof *o);
+  o->maxiter = 10000;                 // nmf.r:13, test_nmf.r:27
+  o->stop_rule = NMFC_STOP_REF_COMPAT;
+  o->label_rule = NMFC_LABEL_ARGMAX;
+  o->seed = 123;                      // nmf.r:13
+  o->min_init = 0;                    // setdefaultopts.c:42-43
+  o->max_init = 1;
+  o->job_begin = 0;
+  o->job_end = -1;
+  o->check_every = 16;
+  o->verbose = 0;
+}
+
+nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a_on_device) {
+  if (!A || m <= 0 || n <= 0) {
+    set_err("nmfc_engine_create: bad arguments (A=%p m=%d n=%d)", (const void*)A, m, n);
+    return nullptr;
+  }
+  nmfc_engine* e = new nmfc_engine();
+  auto fail = [&](const char* what, hipError_t err) -> nmfc_engine* {
+    set_err("nmfc_engine_create: %s: %s", what, hipGetErrorString(err));
+    nmfc_engine_destroy(e);
+    return nullptr;
+  };
+  hipError_t err;
+  if (device >= 0) {
+    if ((err = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", err);
+  }
+  if ((err = hipGetDevice(&e->dev)) != hipSuccess) return fail("hipGetDevice", err);
+  if ((err = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", err);
+  if ((err = hipHostMalloc((void**)&e->h_stopped, 2 * sizeof(int), 0)) != hipSuccess) return fail("hipHostMalloc", err);
+  e->m = m;
+  e->n = n;
+  e->m_pad = round_up(m, TILE);
+  e->n_pad = round_up(n, BK);
+  e->n_cols_pad = round_up(n, TILE);
+  // fixed gene chunks: a function of m only, so every entry's reduction order is batch-independent
+  e->kchunk = 4096;
+  e->nsplit = (int)((e->m_pad + e->kchunk - 1) / e->kchunk);
+  if (e->Acm.ensure(sizeof(double) * e->n_cols_pad * e->m_pad) || e->Arm.ensure(sizeof(double) * e->m_pad * e->n_pad)) {
+    nmfc_engine_destroy(e);
+    return nullptr;
+  }
+  if ((err = hipMemsetAsync(e->Acm.p, 0, e->Acm.bytes, e->st)) != hipSuccess) return fail("memset", err);
+  if ((err = hipMemsetAsync(e->Arm.p, 0, e->Arm.bytes, e->st)) != hipSuccess) return fail("memset", err);
+  const double* dA = A;
+  DevBuf tmp;
+  if (!a_on_device) {
+    if (tmp.ensure(sizeof(double) * (size_t)m * n)) {
+      nmfc_engine_destroy(e);
+      return nullptr;
+    }
+    if ((err = hipMemcpyAsync(tmp.p, A, sizeof(double) * (size_t)m * n, hipMemcpyHostToDevice, e->st)) != hipSuccess)
+      return fail("upload A", err);
+    dA = tmp.as<double>();
+  }
+  dim3 grid((m + NT - 1) / NT, n);
+  hipLaunchKernelGGL(k_layout_a, grid, dim3(NT), 0, e->st, dA, (long)m, m, n, e->m_pad, e->n_pad, e->Acm.as<double>(),
+                     e->Arm.as<double>());
+  if ((err = hipGetLastError()) != hipSuccess) return fail("k_layout_a", err);
+  if ((err = hipStreamSynchronize(e->st)) != hipSuccess) return fail("sync", err);
+  tmp.release();
+  return e;
+}
+
+void nmfc_engine_destroy(nmfc_engine* e) {
+  if (!e) return;
+  if (e->st) (void)hipStreamSynchronize(e->st);
+  drain_timing(e);
+  for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+  DevBuf* bufs[] = {&e->Acm, &e->Arm, &e->W, &e->H, &e->Gpart, &e->SWpart, &e->SHp, &e->rinfo, &e->stop_iter,
+                    &e->stop_reason, &e->unchanged, &e->classes, &e->n_stopped, &e->prb, &e->pre, &e->pcs, &e->pck,
+                    &e->pcr, &e->initjobs, &e->chunk_job, &e->chunk_idx, &e->jump, &e->labels, &e->slot,
+                    &e->grp_begin, &e->grp_list, &e->counts_tmp, &e->cons_tmp};
+  for (DevBuf* b : bufs) b->release();
+  if (e->h_stopped) (void)hipHostFree(e->h_stopped);
+  if (e->st) (void)hipStreamDestroy(e->st);
+  delete e;
+}
+
+void nmfc_engine_set_timing(nmfc_engine* e, int enable) {
+  if (e) e->timing = enable != 0;
+}
+
+long long nmfc_engine_kernel_time(nmfc_engine* e, int kid, double* ms_out) {
+  if (!e || kid < 0 || kid >= KID_N) return -1;
+  if (ms_out) *ms_out = e->kms[kid];
+  return e->kcount[kid];
+}
+
+double nmfc_engine_kernel_flops(nmfc_engine* e, int kid) {
+  if (!e || kid < 0 || kid >= KID_N) return 0.0;
+  return e->kflops[kid];
+}
+
+int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_sweep_opts* opts_in,
+                    const double* W_init, const double* H_init, nmfc_result* out) {
+  if (!e || !ks || nk <= 0 || R <= 0) {
+    set_err("nmfc_engine_run: bad arguments");
+    return -1;
+  }
+  nmfc_sweep_opts opts;
+  if (opts_in)
+    opts = *opts_in;
+  else
+    nmfc_default_opts(&opts);
+  if (opts.check_every <= 0) opts.check_every = 16;
+  const int m = e->m, n = e->n;
+  for (int q = 0; q < nk; ++q) {
+    // nmf.r:107-108 rejects k = 1; the LDS arrays of k_hupdate hold k <= KMAX.
+    if (ks[q] < 2 || ks[q] > KMAX || ks[q] > n || ks[q] > m) {
+      set_err("nmfc_engine_run: k=%d unsupported (need 2 <= k <= min(%d, m, n))", ks[q], KMAX);
+      return -1;
+    }
+  }
+  if (opts.maxiter < 0) {
+    set_err("nmfc_engine_run: maxiter must be >= 0");
+    return -1;
+  }
+  if (opts.stop_rule < 0 || opts.stop_rule > 2 || opts.label_rule < 0 || opts.label_rule > 1) {
+    set_err("nmfc_engine_run: bad stop or label rule");
+    return -1;
+  }
+  HCHECK(hipSetDevice(e->dev));
+  auto t_start = std::chrono::steady_clock::now();
+  for (int q = 0; q < KID_N; ++q) {
+    e->kms[q] = 0;
+    e->kcount[q] = 0;
+    e->kflops[q] = 0;
+  }
+  const long njobs_all = (long)nk * R;
+  const long jb = std::max(0, opts.job_begin);
+  const long je = (opts.job_end < 0) ? njobs_all : std::min<long>(opts.job_end, njobs_all);
+  if (jb >= je) {
+    set_err("nmfc_engine_run: empty job range [%ld, %ld)", jb, je);
+    return -1;
+  }
+  const int nj = (int)(je - jb);
+
+  // ---- packing: restarts grouped by k (descending), sequential fill of 64-column panels ----
+  std::vector<int> order(nj);
+  for (int i = 0; i < nj; ++i) order[i] = i;
+  auto job_k = [&](int s) { return ks[(jb + s) % nk]; };
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return job_k(a) > job_k(b); });
+  std::vector<RestartInfo> ri(nj);
+  std::vector<int> rslot(nj);                 // restart index -> shard job slot
+  std::vector<int> prb_h, pre_h;
+  int fill = TILE, np = -1;
+  for (int q = 0; q < nj; ++q) {
+    const int s = order[q];
+    const int k = job_k(s);
+    if (fill + k > TILE) {
+      ++np;
+      fill = 0;
+      prb_h.push_back(q);
+      pre_h.push_back(q);
+    }
+    ri[q].col0 = np * TILE + fill;
+    ri[q].k = k;
+    rslot[q] = s;
+    fill += k;
+    pre_h[np] = q + 1;
+  }
+  const int npanels = np + 1;
+  const long Kt_pad = (long)npanels * TILE;
+  std::vector<int> pcs_h(Kt_pad, -1), pck_h(Kt_pad, 0), pcr_h(Kt_pad, -1);
+  for (int q = 0; q < nj; ++q) {
+    const int p = ri[q].col0 / TILE, lc = ri[q].col0 % TILE;
+    for (int a = 0; a < ri[q].k; ++a) {
+      pcs_h[(long)p * TILE + lc + a] = lc;
+      pck_h[(long)p * TILE + lc + a] = ri[q].k;
+      pcr_h[(long)p * TILE + lc + a] = q;
+    }
+  }
+  const int ntj = (int)(e->n_cols_pad / TILE);
+  const int ngt = (int)(e->m_pad / TILE);
+  const long g_ld = e->n_cols_pad;
+  const long g_split = Kt_pad * g_ld;
+  const long sw_split = (long)npanels * TILE * TILE;
+  const long cls_ld = std::max<long>(n, KMAX);
+
+  // ---- device buffers ----
+  if (e->W.ensure(sizeof(double) * Kt_pad * e->m_pad) || e->H.ensure(sizeof(double) * Kt_pad * e->n_pad) ||
+      e->Gpart.ensure(sizeof(double) * g_split * e->nsplit) || e->SWpart.ensure(sizeof(double) * sw_split * e->nsplit) ||
+      e->SHp.ensure(sizeof(double) * sw_split) || e->rinfo.ensure(sizeof(RestartInfo) * nj) ||
+      e->stop_iter.ensure(sizeof(int) * nj) || e->stop_reason.ensure(sizeof(int) * nj) ||
+      e->unchanged.ensure(sizeof(int) * nj) || e->classes.ensure(sizeof(int) * nj * cls_ld) ||
+      e->n_stopped.ensure(sizeof(int)) || e->prb.ensure(sizeof(int) * npanels) || e->pre.ensure(sizeof(int) * npanels) ||
+      e->pcs.ensure(sizeof(int) * Kt_pad) || e->pck.ensure(sizeof(int) * Kt_pad) || e->pcr.ensure(sizeof(int) * Kt_pad) ||
+      e->labels.ensure(sizeof(int32_t) * (size_t)nj * n) || e->slot.ensure(sizeof(int) * nj))
+    return -1;
+  hipStream_t st = e->st;
+  HCHECK(hipMemcpyAsync(e->rinfo.p, ri.data(), sizeof(RestartInfo) * nj, hipMemcpyHostToDevice, st));
+  HCHECK(hipMemcpyAsync(e->prb.p, prb_h.data(), sizeof(int) * npanels, hipMemcpyHostToDevice, st));
+  HCHECK(hipMemcpyAsync(e->pre.p, pre_h.data(), sizeof(int) * npanels, hipMemcpyHostToDevice, st));
+  HCHECK(hipMemcpyAsync(e->pcs.p, pcs_h.data(), sizeof(int) * Kt_pad, hipMemcpyHostToDevice, st));
+  HCHECK(hipMemcpyAsync(e->pck.p, pck_h.data(), sizeof(int) * Kt_pad, hipMemcpyHostToDevice, st));
+  HCHECK(hipMemcpyAsync(e->pcr.p, pcr_h.data(), sizeof(int) * Kt_pad, hipMemcpyHostToDevice, st));
+  HCHECK(hipMemcpyAsync(e->slot.p, rslot.data(), sizeof(int) * nj, hipMemcpyHostToDevice, st));
+  HCHECK(hipMemsetAsync(e->stop_iter.p, 0, sizeof(int) * nj, st));
+  HCHECK(hipMemsetAsync(e->stop_reason.p, 0, sizeof(int) * nj, st));
+  HCHECK(hipMemsetAsync(e->unchanged.p, 0, sizeof(int) * nj, st));
+  HCHECK(hipMemsetAsync(e->classes.p, 0, sizeof(int) * nj * cls_ld, st));   // nmf_mu.c:132 zero start
+  HCHECK(hipMemsetAsync(e->n_stopped.p, 0, sizeof(int), st));
+  HCHECK(hipMemsetAsync(e->W.p, 0, sizeof(double) * Kt_pad * e->m_pad, st));
+  HCHECK(hipMemsetAsync(e->H.p, 0, sizeof(double) * Kt_pad * e->n_pad, st));
+  HCHECK(hipMemsetAsync(e->SHp.p, 0, sizeof(double) * sw_split, st));
+
+  // ---- init ----
+  if (W_init && H_init) {
+    // caller-provided factors, shard-job-major: W_j (m x k), H_j (k x n)
+    std::vector<long> woff(nj + 1, 0), hoff(nj + 1, 0);
+    for (int s = 0; s < nj; ++s) {
+      woff[s + 1] = woff[s] + (long)m * job_k(s);
+      hoff[s + 1] = hoff[s] + (long)job_k(s) * n;
+    }
+    std::vector<double> hrow;
+    for (int q = 0; q < nj; ++q) {
+      const int s = rslot[q], k = ri[q].k;
+      HCHECK(hipMemcpy2DAsync(e->W.as<double>() + (long)ri[q].col0 * e->m_pad, sizeof(double) * e->m_pad,
+                              W_init + woff[s], sizeof(double) * m, sizeof(double) * m, k, hipMemcpyHostToDevice, st));
+      hrow.assign((size_t)k * n, 0.0);
+      for (int j = 0; j < n; ++j)
+        for (int a = 0; a < k; ++a) hrow[(size_t)a * n + j] = H_init[hoff[s] + (long)j * k + a];
+      HCHECK(hipMemcpy2DAsync(e->H.as<double>() + (long)ri[q].col0 * e->n_pad, sizeof(double) * e->n_pad, hrow.data(),
+                              sizeof(double) * n, sizeof(double) * n, k, hipMemcpyHostToDevice, st));
+      HCHECK(hipStreamSynchronize(st));   // hrow is reused
+    }
+  } else {
+    std::vector<InitJob> ij(nj);
+    std::vector<int> cj, ci;
+    int maxch = 1;
+    for (int q = 0; q < nj; ++q) {
+      const int s = rslot[q];
+      const long total = (long)m * ri[q].k + (long)ri[q].k * n;
+      const int nch = (int)((total + RCHUNK - 1) / RCHUNK);
+      ij[q].seed = (uint32_t)(opts.seed + (uint32_t)(jb + s));   // job seed = seed + job_id - 1
+      ij[q].col0 = ri[q].col0;
+      ij[q].k = ri[q].k;
+      ij[q].nchunks = nch;
+      maxch = std::max(maxch, nch);
+      for (int c = 0; c < nch; ++c) {
+        cj.push_back(q);
+        ci.push_back(c);
+      }
+    }
+    if (maxch > e->jump_chunks) {
+      std::vector<uint32_t> tab = make_jump_table(maxch);
+      if (e->jump.ensure(sizeof(uint32_t) * tab.size())) return -1;
+      HCHECK(hipMemcpyAsync(e->jump.p, tab.data(), sizeof(uint32_t) * tab.size(), hipMemcpyHostToDevice, st));
+      HCHECK(hipStreamSynchronize(st));
+      e->jump_chunks = maxch;
+    }
+    if (e->initjobs.ensure(sizeof(InitJob) * nj) || e->chunk_job.ensure(sizeof(int) * cj.size()) ||
+        e->chunk_idx.ensure(sizeof(int) * ci.size()))
+      return -1;
+    HCHECK(hipMemcpyAsync(e->initjobs.p, ij.data(), sizeof(InitJob) * nj, hipMemcpyHostToDevice, st));
+    HCHECK(hipMemcpyAsync(e->chunk_job.p, cj.data(), sizeof(int) * cj.size(), hipMemcpyHostToDevice, st));
+    HCHECK(hipMemcpyAsync(e->chunk_idx.p, ci.data(), sizeof(int) * ci.size(), hipMemcpyHostToDevice, st));
+    const int total_chunks = (int)cj.size();
+    {
+      TimedLaunch tl(e, KID_INIT);
+      hipLaunchKernelGGL(k_init, dim3((total_chunks + NT - 1) / NT), dim3(NT), 0, st, e->initjobs.as<InitJob>(),
+                         e->chunk_job.as<int>(), e->chunk_idx.as<int>(), total_chunks, e->jump.as<uint32_t>(), m, n,
+                         e->m_pad, e->n_pad, opts.min_init, opts.max_init, e->W.as<double>(), e->H.as<double>());
+    }
+    HCHECK(hipGetLastError());
+    HCHECK(hipStreamSynchronize(st));   // host vectors cj/ci go out of scope
+  }
+
+  // ---- iterate ----
+  auto t_iter0 = std::chrono::steady_clock::now();
+  const int grid_wta = e->nsplit * npanels * (ntj + 1);
+  const int grid_ahtw = npanels * ngt;
+  int it = 0, q = 0, checked = 0;
+  int iters_done = 0;
+  hipEvent_t ev[2];
+  HCHECK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+  HCHECK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  for (;;) {
+    if (it < opts.maxiter) {
+      const int chunk = std::min(opts.check_every, opts.maxiter - it);
+      for (int c = 1; c <= chunk; ++c) {
+        const int iter = it + c;
+        {
+          TimedLaunch tl(e, KID_WTA);
+          hipLaunchKernelGGL(k_wta, dim3(grid_wta), dim3(NT), 0, st, e->W.as<double>(), e->Acm.as<double>(), e->m_pad,
+                             npanels, ntj, e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->stop_iter.as<int>(), iter,
+                             e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_split);
+        }
+        {
+          TimedLaunch tl(e, KID_HUPD);
+          hipLaunchKernelGGL(k_hupdate, dim3(nj), dim3(NT), 0, st, iter, opts.maxiter, opts.stop_rule,
+                             e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, e->nsplit,
+                             e->SWpart.as<double>(), sw_split, e->H.as<double>(), e->SHp.as<double>(),
+                             e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->unchanged.as<int>(),
+                             e->classes.as<int>(), cls_ld, e->n_stopped.as<int>());
+        }
+        {
+          TimedLaunch tl(e, KID_AHTW);
+          hipLaunchKernelGGL(k_ahtw, dim3(grid_ahtw), dim3(NT), 0, st, iter, e->H.as<double>(), e->n_pad,
+                             e->Arm.as<double>(), e->m_pad, e->W.as<double>(), e->SHp.as<double>(), e->pcs.as<int>(),
+                             e->pck.as<int>(), e->pcr.as<int>(), e->prb.as<int>(), e->pre.as<int>(),
+                             e->stop_iter.as<int>(), ngt);
+        }
+      }
+      HCHECK(hipGetLastError());
+      it += chunk;
+      HCHECK(hipMemcpyAsync(&e->h_stopped[q & 1], e->n_stopped.p, sizeof(int), hipMemcpyDeviceToHost, st));
+      HCHECK(hipEventRecord(ev[q & 1], st));
+      ++q;
+    }
+    // consume polls, keeping one chunk in flight while there is more to enqueue
+    const int target = (it < opts.maxiter) ? q - 1 : q;
+    bool done = false;
+    while (checked < target) {
+      HCHECK(hipEventSynchronize(ev[checked & 1]));
+      if (e->h_stopped[checked & 1] >= nj) done = true;
+      ++checked;
+    }
+    if (e->timing) drain_timing(e);
+    if (done || (it >= opts.maxiter && checked == q)) break;
+  }
+  HCHECK(hipStreamSynchronize(st));
+  (void)hipEventDestroy(ev[0]);
+  (void)hipEventDestroy(ev[1]);
+  iters_done = it;
+  auto t_iter1 = std::chrono::steady_clock::now();
+
+  // ---- labels, counts ----
+  {
+    TimedLaunch tl(e, KID_LABEL);
+    hipLaunchKernelGGL(k_labels, dim3((n + NT - 1) / NT, nj), dim3(NT), 0, st, e->rinfo.as<RestartInfo>(),
+                       e->slot.as<int>(), e->H.as<double>(), e->n_pad, n, opts.label_rule, e->labels.as<int32_t>());
+  }
+  HCHECK(hipGetLastError());
+  std::vector<int> gb(nk + 1, 0), gl;
+  for (int g = 0; g < nk; ++g) {
+    gb[g] = (int)gl.size();
+    for (int s = 0; s < nj; ++s)
+      if ((jb + s) % nk == g) gl.push_back(s);
+  }
+  gb[nk] = (int)gl.size();
+  const size_t cnt_len = (size_t)nk * n * n;
+  if (out && (out->counts || out->consensus)) {
+    if (e->grp_begin.ensure(sizeof(int) * (nk + 1)) || e->grp_list.ensure(sizeof(int) * std::max<size_t>(gl.size(), 1)))
+      return -1;
+    HCHECK(hipMemcpyAsync(e->grp_begin.p, gb.data(), sizeof(int) * (nk + 1), hipMemcpyHostToDevice, st));
+    if (!gl.empty()) HCHECK(hipMemcpyAsync(e->grp_list.p, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice, st));
+    int32_t* dcounts;
+    if (out->counts && out->counts_on_device) {
+      dcounts = out->counts;
+    } else {
+      if (e->counts_tmp.ensure(sizeof(int32_t) * cnt_len)) return -1;
+      dcounts = e->counts_tmp.as<int32_t>();
+    }
+    {
+      TimedLaunch tl(e, KID_LABEL);
+      hipLaunchKernelGGL(k_counts, dim3((n + 15) / 16, (n + 15) / 16, nk), dim3(NT), 0, st, e->labels.as<int32_t>(),
+                         e->grp_begin.as<int>(), e->grp_list.as<int>(), n, dcounts);
+    }
+    HCHECK(hipGetLastError());
+    if (out->consensus) {
+      if (e->cons_tmp.ensure(sizeof(double) * cnt_len)) return -1;
+      hipLaunchKernelGGL(k_divide, dim3((unsigned)((cnt_len + NT - 1) / NT)), dim3(NT), 0, st, dcounts, (double)R,
+                         (long)cnt_len, e->cons_tmp.as<double>());
+      HCHECK(hipGetLastError());
+      HCHECK(hipMemcpyAsync(out->consensus, e->cons_tmp.p, sizeof(double) * cnt_len, hipMemcpyDeviceToHost, st));
+    }
+    if (out->counts && !out->counts_on_device)
+      HCHECK(hipMemcpyAsync(out->counts, dcounts, sizeof(int32_t) * cnt_len, hipMemcpyDeviceToHost, st));
+  }
+  std::vector<int> si(nj), sr(nj);
+  HCHECK(hipMemcpyAsync(si.data(), e->stop_iter.p, sizeof(int) * nj, hipMemcpyDeviceToHost, st));
+  HCHECK(hipMemcpyAsync(sr.data(), e->stop_reason.p, sizeof(int) * nj, hipMemcpyDeviceToHost, st));
+  if (out && out->labels)
+    HCHECK(hipMemcpyAsync(out->labels, e->labels.p, sizeof(int32_t) * (size_t)nj * n, hipMemcpyDeviceToHost, st));
+  HCHECK(hipStreamSynchronize(st));
+  if (e->timing) drain_timing(e);
+
+  long long tot_iters = 0;
+  int max_it = 0;
+  double fl_wta = 0, fl_ahtw = 0;
+  for (int qq = 0; qq < nj; ++qq) {
+    const int itr = si[qq] ? si[qq] : iters_done;
+    tot_iters += itr;
+    max_it = std::max(max_it, itr);
+    const double k = ri[qq].k;
+    // algorithmic flops (nmf_mu.c:174-202 at 2*M*N*K each): W^T A + W^T W  |  A h^T + W0 (h h^T)
+    fl_wta += (double)itr * (2.0 * m * n * k + 2.0 * m * k * k);
+    fl_ahtw += (double)itr * (2.0 * m * n * k + 2.0 * m * k * k);
+    if (out && out->iters) out->iters[rslot[qq]] = itr;
+    if (out && out->stopped_early) out->stopped_early[rslot[qq]] = (sr[qq] == 1);
+  }
+  if (e->kcount[KID_WTA]) e->kflops[KID_WTA] = fl_wta / e->kcount[KID_WTA];
+  if (e->kcount[KID_AHTW]) e->kflops[KID_AHTW] = fl_ahtw / e->kcount[KID_AHTW];
+
+  if (out && (out->W || out->H)) {
+    std::vector<long> woff(nj + 1, 0), hoff(nj + 1, 0);
+    for (int s = 0; s < nj; ++s) {
+      woff[s + 1] = woff[s] + (long)m * job_k(s);
+      hoff[s + 1] = hoff[s] + (long)job_k(s) * n;
+    }
+    std::vector<double> hrow;
+    for (int qq = 0; qq < nj; ++qq) {
+      const int s = rslot[qq], k = ri[qq].k;
+      if (out->W)
+        HCHECK(hipMemcpy2DAsync(out->W + woff[s], sizeof(double) * m, e->W.as<double>() + (long)ri[qq].col0 * e->m_pad,
+                                sizeof(double) * e->m_pad, sizeof(double) * m, k, hipMemcpyDeviceToHost, st));
+      if (out->H) {
+        hrow.assign((size_t)k * n, 0.0);
+        HCHECK(hipMemcpy2DAsync(hrow.data(), sizeof(double) * n, e->H.as<double>() + (long)ri[qq].col0 * e->n_pad,
+                                sizeof(double) * e->n_pad, sizeof(double) * n, k, hipMemcpyDeviceToHost, st));
+        HCHECK(hipStreamSynchronize(st));
+        for (int j = 0; j < n; ++j)
+          for (int a = 0; a < k; ++a) out->H[hoff[s] + (long)j * k + a] = hrow[(size_t)a * n + j];
+      }
+    }
+    HCHECK(hipStreamSynchronize(st));
+  }
+  auto t_end = std::chrono::steady_clock::now();
+  if (out) {
+    out->seconds_total = std::chrono::duration<double>(t_end - t_start).count();
+    out->seconds_iterate = std::chrono::duration<double>(t_iter1 - t_iter0).count();
+    out->restart_iterations = tot_iters;
+    out->max_iter_run = max_it;
+  }
+  if (opts.verbose) {
+    fprintf(stderr, "[nmfc] %d restarts in %d panels, %d iterations enqueued, max %d, mean %.1f, %.3f s\n", nj, npanels,
+            iters_done, max_it, (double)tot_iters / nj, std::chrono::duration<double>(t_end - t_start).count());
+  }
+  return 0;
+}
+
+int nmfc_consensus(const double* Hs, int k, int n, int R, int label_rule, int32_t* labels, int32_t* counts,
+                   double* consensus) {
+  if (!Hs || k < 1 || n < 1 || R < 1 || label_rule < 0 || label_rule > 1) {
+    set_err("nmfc_consensus: bad arguments");
+    return -1;
+  }
+  std::vector<double> hrows((size_t)R * k * n);
+  for (int r = 0; r < R; ++r)
+    for (int j = 0; j < n; ++j)
+      for (int a = 0; a < k; ++a) hrows[((size_t)r * k + a) * n + j] = Hs[(size_t)r * k * n + (size_t)j * k + a];
+  std::vector<RestartInfo> ri(R);
+  std::vector<int> slot(R), gb = {0, R};
+  for (int r = 0; r < R; ++r) {
+    ri[r].col0 = r * k;
+    ri[r].k = k;
+    slot[r] = r;
+  }
+  DevBuf dH, dri, dslot, dgb, dlab, dcnt, dcons;
+  if (dH.ensure(sizeof(double) * hrows.size()) || dri.ensure(sizeof(RestartInfo) * R) || dslot.ensure(sizeof(int) * R) ||
+      dgb.ensure(sizeof(int) * 2) || dlab.ensure(sizeof(int32_t) * (size_t)R * n) ||
+      dcnt.ensure(sizeof(int32_t) * (size_t)n * n) || dcons.ensure(sizeof(double) * (size_t)n * n))
+    return -1;
+  HCHECK(hipMemcpy(dH.p, hrows.data(), sizeof(double) * hrows.size(), hipMemcpyHostToDevice));
+  HCHECK(hipMemcpy(dri.p, ri.data(), sizeof(RestartInfo) * R, hipMemcpyHostToDevice));
+  HCHECK(hipMemcpy(dslot.p, slot.data(), sizeof(int) * R, hipMemcpyHostToDevice));
+  HCHECK(hipMemcpy(dgb.p, gb.data(), sizeof(int) * 2, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_labels, dim3((n + NT - 1) / NT, R), dim3(NT), 0, 0, dri.as<RestartInfo>(), dslot.as<int>(),
+                     dH.as<double>(), (long)n, n, label_rule, dlab.as<int32_t>());
+  HCHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_counts, dim3((n + 15) / 16, (n + 15) / 16, 1), dim3(NT), 0, 0, dlab.as<int32_t>(), dgb.as<int>(),
+                     dslot.as<int>(), n, dcnt.as<int32_t>());
+  HCHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_divide, dim3((unsigned)(((size_t)n * n + NT - 1) / NT)), dim3(NT), 0, 0, dcnt.as<int32_t>(),
+                     (double)R, (long)n * n, dcons.as<double>());
+  HCHECK(hipGetLastError());
+  if (labels) HCHECK(hipMemcpy(labels, dlab.p, sizeof(int32_t) * (size_t)R * n, hipMemcpyDeviceToHost));
+  if (counts) HCHECK(hipMemcpy(counts, dcnt.p, sizeof(int32_t) * (size_t)n * n, hipMemcpyDeviceToHost));
+  if (consensus) HCHECK(hipMemcpy(consensus, dcons.p, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToHost));
+  HCHECK(hipDeviceSynchronize());
+  return 0;
+}
+
+int nmfc_sweep(const double* A, int m, int n, const int* ks, int nk, int R, const nmfc_sweep_opts* opts,
+               nmfc_result* out) {
+  nmfc_engine* e = nmfc_engine_create(-1, A, m, n, 0);
+  if (!e) return -1;
+  int rc = nmfc_engine_run(e, ks, nk, R, opts, nullptr, nullptr, out);
+  nmfc_engine_destroy(e);
+  return rc;
+}
+
+}  // extern "C"

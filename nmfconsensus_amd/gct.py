@@ -1,0 +1,76 @@
+"""GCT 1.2 dataset I/O -- mirror of nmf.r's read.gct / write.gct / read.dataset.
+
+read.gct  (nmf.r:371-377): read.delim(skip=2, header=T, row.names=1) then drop the Description column.
+write.gct (nmf.r:379-408): "#1.2", dims, a header "Name\tDescription\t1..ncol" + column names, then rows
+                           with the row name repeated as Name and Description.
+Values are parsed with Python's correctly rounded float(); R's own R_strtod is not pinned here
+(no R in the image), see DESIGN.md.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+class GCT:
+    """A parsed GCT: `data` is an (genes x samples) float64 array in Fortran order (libnmf's layout)."""
+
+    def __init__(self, data: np.ndarray, row_names: list[str], col_names: list[str]):
+        self.data = np.asfortranarray(data, dtype=np.float64)
+        self.row_names = list(row_names)
+        self.col_names = list(col_names)
+
+    @property
+    def shape(self):
+        return self.data.shape
+
+
+def read_gct(path: str) -> GCT:
+    with open(path, "r") as f:
+        lines = f.read().splitlines()
+    if not lines or not lines[0].startswith("#1.2"):
+        raise ValueError(f"{path}: not a GCT 1.2 file")
+    dims = lines[1].split("\t")
+    nrow, ncol = int(dims[0]), int(dims[1])
+    header = lines[2].split("\t")
+    col_names = header[2:2 + ncol]
+    rows, names = [], []
+    for ln in lines[3:]:
+        if not ln.strip():
+            continue  # blank.lines.skip=T
+        parts = ln.split("\t")
+        names.append(parts[0])
+        rows.append([float(x) for x in parts[2:2 + ncol]])
+    data = np.array(rows, dtype=np.float64)
+    if data.shape != (nrow, ncol):
+        raise ValueError(f"{path}: header says {nrow}x{ncol}, body has {data.shape}")
+    return GCT(data, names, col_names)
+
+
+def read_dataset(path: str) -> GCT:
+    """nmf.r:261-269: dispatch on the file suffix (.gct only; .res is out of scope)."""
+    if path.lower().endswith(".gct"):
+        return read_gct(path)
+    raise ValueError("Input is not a res or gct file.")
+
+
+def _fmt(v) -> str:
+    if isinstance(v, (float, np.floating)):
+        return repr(float(v)) if not float(v).is_integer() else str(int(v))
+    return str(v)
+
+
+def write_gct(data, row_names, col_names, path: str) -> None:
+    """nmf.r:379-408 layout."""
+    data = np.asarray(data)
+    if data.ndim == 1:
+        data = data[:, None]
+    nr, nc = data.shape
+    with open(path, "w") as f:
+        f.write("#1.2\n")
+        f.write(f"{nr}\t{nc}\n")
+        f.write("Name\tDescription\t" + "\t".join(str(i + 1) for i in range(nc)))
+        for c in col_names:
+            f.write("\t" + str(c))
+        f.write("\n")
+        for i in range(nr):
+            f.write(str(row_names[i]) + "\t" + str(row_names[i]) + "\t" + "\t".join(_fmt(v) for v in data[i]) + "\n")

@@ -1,0 +1,192 @@
+"""GPU parity: the HIP engine (libnmf.so) against the reference's golden vectors and the oracle.
+
+Bars (BASELINE.json north_star): init, iteration counts, labels, connectivity and consensus
+bit-exact; W/H within 1e-9 relative Frobenius error after a fixed iteration count.
+"""
+import numpy as np
+import pytest
+
+from conftest import relfro
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-9   # north_star: per-restart W/H within 1e-9 relative Frobenius error
+
+
+@pytest.fixture(scope="module")
+def gct_engine(golden):
+    from nmfconsensus_amd.nmf import Engine
+    eng = Engine(golden["A_gct"])
+    yield eng
+    eng.close()
+
+
+def test_mfma_layout_and_small_gemm(golden):
+    # a tiny case through the whole path: m=5, n=4, k=2 with the reference's generateMatrix init
+    from nmfconsensus_amd.nmf import Engine
+    from pyoracle import Oracle, STOP_FIXED
+    A = np.asfortranarray(np.arange(1, 21, dtype=np.float64).reshape(5, 4) % 7 + 0.5)
+    O = Oracle()
+    with Engine(A) as eng:
+        r0 = eng.run([2], 1, maxiter=0, seed=123, want_factors=True, want_counts=False)
+        assert np.array_equal(r0.W[0], golden["init_small_W"])
+        assert np.array_equal(r0.H[0], golden["init_small_H"])
+        for T in (1, 2, 7, 50):
+            r = eng.run([2], 1, maxiter=T, seed=123, stop_rule=0, want_factors=True, want_counts=False)
+            Wo, Ho, it = O.nmf_mu(A, golden["init_small_W"], golden["init_small_H"], T, STOP_FIXED)
+            assert r.iters[0] == T
+            assert relfro(r.W[0], Wo) < TOL and relfro(r.H[0], Ho) < TOL, T
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 5])
+def test_init_stream_bitexact(gct_engine, golden, k):
+    r = gct_engine.run([k], 1, maxiter=0, seed=123, want_factors=True, want_counts=False)
+    assert np.array_equal(r.W[0], golden[f"init_k{k}_W"])
+    assert np.array_equal(r.H[0], golden[f"init_k{k}_H"])
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 5])
+@pytest.mark.parametrize("T", [2, 10, 200, 398])
+def test_fixed_iterations(gct_engine, golden, k, T):
+    r = gct_engine.run([k], 1, maxiter=T, seed=123, stop_rule=0, want_factors=True, want_counts=False)
+    assert r.iters[0] == T
+    assert relfro(r.W[0], golden[f"fixed_k{k}_T{T}_W"]) < TOL
+    assert relfro(r.H[0], golden[f"fixed_k{k}_T{T}_H"]) < TOL
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 5])
+def test_ref_compat_exit(gct_engine, golden, k):
+    r = gct_engine.run([k], 1, maxiter=10000, seed=123, stop_rule=1, want_factors=True, want_counts=False)
+    assert r.iters[0] == int(golden[f"refc_k{k}_iter"])
+    assert r.stopped_early[0] == 1
+    assert relfro(r.W[0], golden[f"refc_k{k}_W"]) < TOL
+    assert relfro(r.H[0], golden[f"refc_k{k}_H"]) < TOL
+
+
+def test_user_init_path(gct_engine, golden):
+    # caller-provided W0/H0 (the .C("nmf_mu") path) gives the same result as the generated init
+    k, T = 3, 10
+    r = gct_engine.run([k], 1, maxiter=T, stop_rule=0, W_init=[golden[f"init_k{k}_W"]],
+                       H_init=[golden[f"init_k{k}_H"]], want_factors=True, want_counts=False)
+    assert relfro(r.W[0], golden[f"fixed_k{k}_T{T}_W"]) < TOL
+    assert relfro(r.H[0], golden[f"fixed_k{k}_T{T}_H"]) < TOL
+
+
+@pytest.mark.parametrize("rule,key", [(0, "argmax"), (1, "rorder")])
+def test_c1_sweep_consensus_bitexact(gct_engine, golden, rule, key):
+    ks = [int(x) for x in golden["c1_ks"]]
+    R = int(golden["c1_R"])
+    r = gct_engine.run(ks, R, maxiter=10000, seed=int(golden["c1_seed"]), stop_rule=1, label_rule=rule,
+                       want_factors=True)
+    assert np.array_equal(r.iters, golden["c1_iters"])
+    assert np.array_equal(r.labels, golden[f"c1_labels_{key}"])
+    for i, k in enumerate(ks):
+        assert np.array_equal(r.counts[i], golden[f"c1_counts_{key}_k{k}"])
+        assert np.array_equal(r.consensus[i], golden[f"c1_counts_{key}_k{k}"] / R)
+    jk = golden["c1_job_k"]
+    for k in ks:
+        idx = np.where(jk == k)[0]
+        for q, j in enumerate(idx):
+            assert relfro(r.H[j], golden[f"c1_H_k{k}"][q]) < TOL
+
+
+def test_shard_and_batch_invariance(gct_engine, golden):
+    ks = [2, 3, 4, 5]
+    R = 20
+    full = gct_engine.run(ks, R, maxiter=600, seed=7, stop_rule=1, want_factors=True)
+    a = gct_engine.run(ks, R, maxiter=600, seed=7, stop_rule=1, job_begin=0, job_end=37, want_factors=True)
+    b = gct_engine.run(ks, R, maxiter=600, seed=7, stop_rule=1, job_begin=37, job_end=80, want_factors=True)
+    assert np.array_equal(a.counts + b.counts, full.counts)
+    assert np.array_equal(np.concatenate([a.iters, b.iters]), full.iters)
+    for j in range(80):
+        src = a if j < 37 else b
+        jj = j if j < 37 else j - 37
+        assert np.array_equal(src.W[jj], full.W[j])   # bit-identical: arithmetic independent of placement
+        assert np.array_equal(src.H[jj], full.H[j])
+    # the same job alone in a batch of one
+    one = gct_engine.run(ks, R, maxiter=600, seed=7, stop_rule=1, job_begin=41, job_end=42, want_factors=True)
+    assert np.array_equal(one.W[0], full.W[41]) and np.array_equal(one.H[0], full.H[41])
+
+
+def test_argmax_stable_rule(gct_engine, golden, oracle):
+    A = golden["A_gct"]
+    for k in (2, 4):
+        W0, H0 = golden[f"init_k{k}_W"], golden[f"init_k{k}_H"]
+        Wo, Ho, ito = oracle.nmf_mu(A, W0, H0, 10000, 2)
+        r = gct_engine.run([k], 1, maxiter=10000, seed=123, stop_rule=2, want_factors=True, want_counts=False)
+        assert r.iters[0] == ito
+        assert relfro(r.W[0], Wo) < TOL and relfro(r.H[0], Ho) < TOL
+
+
+def test_nmf_mu_abi(golden):
+    from nmfconsensus_amd import libnmf
+    A = golden["A_gct"]
+    k = 4
+    out = libnmf.nmf_mu(A, golden[f"init_k{k}_W"], golden[f"init_k{k}_H"], 10000)
+    assert out["maxiter"] == int(golden[f"refc_k{k}_iter"])
+    assert relfro(out["w0"], golden[f"refc_k{k}_W"]) < TOL
+    assert relfro(out["h0"], golden[f"refc_k{k}_H"]) < TOL
+    assert out["ret"] == 0
+    # cap reached: *maxiter unchanged; odd counts still leave the result in the caller's buffers
+    out = libnmf.nmf_mu(A, golden[f"init_k{k}_W"], golden[f"init_k{k}_H"], 10)
+    assert out["maxiter"] == 10
+    assert relfro(out["h0"], golden[f"fixed_k{k}_T10_H"]) < TOL
+
+
+def test_nmf_mu_odd_iterations(golden, oracle):
+    from nmfconsensus_amd import libnmf
+    A = golden["A_gct"]
+    W0, H0 = golden["init_k3_W"], golden["init_k3_H"]
+    out = libnmf.nmf_mu(A, W0, H0, 7)
+    Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, 7, 0)
+    assert out["maxiter"] == 7
+    assert relfro(out["w0"], Wo) < TOL and relfro(out["h0"], Ho) < TOL
+
+
+def test_norm_and_maxchange(golden):
+    from nmfconsensus_amd import libnmf
+    v, d = libnmf.calculateNorm(golden["norm_a"], golden["norm_w"], golden["norm_h"])
+    assert abs(v - float(golden["norm_value"])) <= 1e-12 * abs(float(golden["norm_value"]))
+    assert relfro(d, golden["norm_d"]) < 1e-13
+    v, m0 = libnmf.calculateMaxchange(golden["maxchange_mat"], golden["maxchange_mat0"])
+    assert v == float(golden["maxchange_value"])
+    assert np.array_equal(m0, golden["maxchange_mat0_after"])
+
+
+def test_consensus_entry_matches_sweep(gct_engine, golden):
+    from nmfconsensus_amd.nmf import computeConsensusMatrixFromClusterings
+    k = 3
+    C = computeConsensusMatrixFromClusterings([{"H": h} for h in golden[f"c1_H_k{k}"]])
+    assert np.array_equal(C, golden[f"c1_counts_argmax_k{k}"] / 20)
+
+
+@pytest.mark.parametrize("m,n,ks", [(3001, 150, [2, 7, 10, 16]), (64, 64, [2, 16]), (97, 33, [5]),
+                                    (130, 17, [2, 3])])
+def test_ragged_shapes_vs_oracle(oracle, m, n, ks):
+    from nmfconsensus_amd.nmf import Engine
+    rng = np.random.default_rng(m * 1000 + n)
+    A = np.asfortranarray(rng.random((m, n)) * 3.0)
+    A[5, :] = 0.0   # a zero gene row
+    A[:, 3] = 0.0   # a zero sample column
+    T = 12
+    with Engine(A) as eng:
+        r = eng.run(ks, 2, maxiter=T, seed=99, stop_rule=0, want_factors=True)
+    for j in range(len(ks) * 2):
+        k = ks[j % len(ks)]
+        W0, H0 = oracle.init_restart(99 + j, m, n, k)
+        Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, T, 0)
+        assert relfro(r.W[j], Wo) < TOL and relfro(r.H[j], Ho) < TOL, (m, n, k)
+        assert np.all(r.H[j][:, 3] == 0.0)
+
+
+def test_full_size_c3_shape_vs_oracle(oracle):
+    # BASELINE config C3 shape (20000 x 500), k = 10, a few fixed iterations against the oracle
+    from nmfconsensus_amd.nmf import Engine
+    rng = np.random.default_rng(3)
+    m, n, k, T = 20000, 500, 10, 4
+    A = np.asfortranarray(rng.random((m, n)) * 5.0)
+    with Engine(A) as eng:
+        r = eng.run([k], 1, maxiter=T, seed=20261015, stop_rule=0, want_factors=True, want_counts=False)
+    W0, H0 = oracle.init_restart(20261015, m, n, k)
+    Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, T, 0)
+    assert relfro(r.W[0], Wo) < TOL and relfro(r.H[0], Ho) < TOL

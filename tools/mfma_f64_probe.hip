@@ -1,0 +1,88 @@
+// Probe: fp64 MFMA (v_mfma_f64_16x16x4_f64) operand/result lane maps and issue rate on gfx950,
+// plus the fp64 VALU FMA rate. Standalone; not part of the product library.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cmath>
+typedef double d4 __attribute__((ext_vector_type(4)));
+#define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP %s at %d\n",hipGetErrorString(e),__LINE__);exit(1);}}while(0)
+
+__global__ void layout_k(const double* A, const double* B, double* C) {
+  int l = threadIdx.x;
+  d4 acc = {0, 0, 0, 0};
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(l & 15) * 4 + (l >> 4)], B[(l >> 4) * 16 + (l & 15)], acc, 0, 0, 0);
+  for (int r = 0; r < 4; r++) C[l * 4 + r] = acc[r];
+}
+
+template <int NACC>
+__global__ void rate_k(double* out, int iters, double seed) {
+  d4 acc[NACC];
+  for (int i = 0; i < NACC; i++) acc[i] = (d4){seed, seed, seed, seed};
+  double a = seed + threadIdx.x * 1e-3, b = seed - threadIdx.x * 1e-3;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int i = 0; i < NACC; i++) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
+  }
+  double s = 0;
+  for (int i = 0; i < NACC; i++) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+__global__ void valu_k(double* out, int iters, double seed) {
+  double x[8];
+  for (int i = 0; i < 8; i++) x[i] = seed + i + threadIdx.x;
+  double m = 1.0000001, c = 1e-9;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = fma(x[i], m, c);
+  }
+  double s = 0;
+  for (int i = 0; i < 8; i++) s += x[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+int main() {
+  double hA[64], hB[64], hC[256];
+  for (int i = 0; i < 16; i++) for (int k = 0; k < 4; k++) hA[i * 4 + k] = (i + 1) * 1.0 + (k + 1) * 0.001;
+  for (int k = 0; k < 4; k++) for (int j = 0; j < 16; j++) hB[k * 16 + j] = (k == 0 ? 1.0 : 0.0) * (j + 1) + (k + 1) * 100.0 * (j == 3);
+  double *dA, *dB, *dC;
+  CK(hipMalloc(&dA, 64 * 8)); CK(hipMalloc(&dB, 64 * 8)); CK(hipMalloc(&dC, 256 * 8));
+  CK(hipMemcpy(dA, hA, 64 * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dB, hB, 64 * 8, hipMemcpyHostToDevice));
+  layout_k<<<1, 64>>>(dA, dB, dC);
+  CK(hipMemcpy(hC, dC, 256 * 8, hipMemcpyDeviceToHost));
+  double ref[16][16];
+  for (int i = 0; i < 16; i++) for (int j = 0; j < 16; j++) { double s = 0; for (int k = 0; k < 4; k++) s += hA[i * 4 + k] * hB[k * 16 + j]; ref[i][j] = s; }
+  int ok_guide = 1, ok_f32 = 1;
+  for (int l = 0; l < 64; l++) for (int r = 0; r < 4; r++) {
+    int col = l & 15;
+    int row_g = (l >> 4) + 4 * r, row_f = (l >> 4) * 4 + r;
+    if (fabs(hC[l * 4 + r] - ref[row_g][col]) > 1e-9) ok_guide = 0;
+    if (fabs(hC[l * 4 + r] - ref[row_f][col]) > 1e-9) ok_f32 = 0;
+  }
+  printf("layout: row=(lane>>4)+4*reg: %s ; row=(lane>>4)*4+reg: %s\n", ok_guide ? "MATCH" : "no", ok_f32 ? "MATCH" : "no");
+
+  double* dout; CK(hipMalloc(&dout, 1 << 24));
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  int iters = 4000; float ms;
+  for (int rep = 0; rep < 2; rep++) {
+    int blocks = 256 * 4, threads = 256;
+    CK(hipEventRecord(e0)); rate_k<4><<<blocks, threads>>>(dout, iters, 1.0); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    double fl = (double)blocks * (threads / 64) * iters * 4 * 2048.0;
+    printf("mfma f64 16x16x4, 4 acc, %d WGx%d: %.3f ms  %.2f TFLOP/s\n", blocks, threads, ms, fl / ms / 1e9);
+    CK(hipEventRecord(e0)); rate_k<1><<<blocks, threads>>>(dout, iters, 1.0); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    fl = (double)blocks * (threads / 64) * iters * 1 * 2048.0;
+    printf("mfma f64 16x16x4, 1 acc: %.3f ms  %.2f TFLOP/s\n", ms, fl / ms / 1e9);
+    CK(hipEventRecord(e0)); rate_k<4><<<256, 64>>>(dout, iters, 1.0); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    fl = 256.0 * iters * 4 * 2048.0;
+    printf("mfma f64 one wave/CU 4 acc: %.3f ms -> %.1f cycles/mfma @2.4GHz\n", ms, ms * 1e-3 * 2.4e9 / (iters * 4.0));
+    CK(hipEventRecord(e0)); valu_k<<<blocks, threads>>>(dout, iters, 1.0); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    fl = (double)blocks * threads * iters * 8 * 2.0;
+    printf("valu fma f64: %.3f ms  %.2f TFLOP/s\n", ms, fl / ms / 1e9);
+  }
+  return 0;
+}
