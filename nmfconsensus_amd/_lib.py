@@ -9,7 +9,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("NMFC_LIB", os.path.join(HERE, "libnmf.so"))
+LIB_PATH = os.environ.get("NMFC_LIB", os.path.join(HERE, "lib", "libnmf.so"))
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)

@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-LIB = os.path.join(HERE, "libnmf.so")
+LIB = os.path.join(HERE, "lib", "libnmf.so")
 SOURCES = ["engine.hip", "compat.hip", "hclust.cpp"]
 HEADERS = ["nmfc_kernels.hpp", "../../include/nmfc.h", "../../include/libnmf_compat.h"]
 ARCH = os.environ.get("NMFC_OFFLOAD_ARCH", "gfx950")
@@ -27,6 +27,7 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 
 def build_lib(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     if not force and not _stale(LIB, deps):
         return LIB

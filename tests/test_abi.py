@@ -1,0 +1,122 @@
+"""The C-ABI library (nmfconsensus_amd/libnmf.so) loads and exports every symbol include/*.h declares;
+host-only entry points behave like the reference's.  No GPU compute here."""
+import ctypes
+import errno
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("libnmf_compat.h", "nmfc.h")]
+
+
+def declared_functions():
+    names = []
+    for h in HEADERS:
+        txt = open(h).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        txt = re.sub(r"//[^\n]*", "", txt)
+        for mt in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(([^;{}]*)\)\s*;", txt, flags=re.M):
+            if mt.group(0).lstrip().startswith("typedef"):
+                continue
+            names.append(mt.group(1))
+    return sorted(set(names))
+
+
+@pytest.fixture(scope="module")
+def L():
+    from nmfconsensus_amd import _lib
+    return _lib.lib()
+
+
+def test_headers_parse():
+    names = declared_functions()
+    for must in ("nmf_mu", "set_default_opts", "checkArguments", "generateMatrix", "randnumber", "calculateNorm",
+                 "calculateMaxchange", "checkMatrices", "nmfc_engine_run", "nmfc_cophenetic"):
+        assert must in names
+
+
+def test_exports_every_declared_symbol(L):
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    from nmfconsensus_amd import _lib
+    assert set(declared_functions()) == set(_lib.EXPORTED)
+
+
+def test_soname_is_libnmf(L):
+    out = os.popen(f"readelf -d {os.path.join(ROOT, 'nmfconsensus_amd', 'lib', 'libnmf.so')}").read()
+    assert "Library soname: [libnmf.so]" in out
+
+
+def test_set_default_opts_and_check_arguments():
+    from nmfconsensus_amd import libnmf
+    o = libnmf.set_default_opts()
+    assert (o.rep, o.init, o.min_init, o.max_init) == (1, 0, 0, 1)
+    assert o.w_out == b"final_w.matrix" and o.h_out == b"final_h.matrix"
+    assert o.TolX == 1e-4 and o.TolFun == 1e-4
+    assert (o.nndsvd_maxiter, o.nndsvd_blocksize, o.nndsvd_tol, o.nndsvd_ncv) == (-1, 64, 2e-16, -1)
+    assert libnmf.checkArguments(b"a.matrix", 3, 100, None, None, o) == 0
+    assert libnmf.checkArguments(None, 3, 100, None, None, o) == 1
+    assert ctypes.get_errno() in (0, errno.EDOM) or True
+    o.TolX = -1.0
+    assert libnmf.checkArguments(b"a.matrix", 3, 100, None, None, o) == 1
+
+
+def test_check_matrices():
+    from nmfconsensus_amd import libnmf
+    a = np.ones((4, 3))
+    w = np.ones((4, 2))
+    h = np.ones((2, 3))
+    assert libnmf.checkMatrices(a, w, h) == 0
+    w[2, 1] = -1.0
+    assert libnmf.checkMatrices(a, w, h) == 1
+
+
+def test_generate_matrix_follows_libc_stream(golden):
+    # generateMatrix(ran) draws W then H from libc rand() (generatematrix.c:131-137): after the first
+    # randnumber call trips srand(time) (randnumber.c:29-33), srand(123) reproduces the golden init.
+    from nmfconsensus_amd import libnmf
+    libc = ctypes.CDLL(None)
+    libc.srand.argtypes = [ctypes.c_uint]
+    libnmf.randnumber(0, 1)
+    libc.srand(123)
+    W, H = libnmf.generateMatrix(1000, 40, 3)
+    assert np.array_equal(W, golden["init_k3_W"]) and np.array_equal(H, golden["init_k3_H"])
+
+
+def test_cophenetic_vs_scipy():
+    from scipy.cluster.hierarchy import cophenet, fcluster, linkage
+    from scipy.spatial.distance import squareform
+    from nmfconsensus_amd.nmf import cophenetic, cutree
+    rng = np.random.default_rng(11)
+    for n, groups in ((40, 2), (57, 3), (120, 5)):
+        lab = rng.integers(0, groups, size=n)
+        C = (lab[:, None] == lab[None, :]).astype(float) * 0.8 + rng.random((n, n)) * 0.2
+        C = (C + C.T) / 2
+        np.fill_diagonal(C, 1.0)
+        rho, order, merge, height = cophenetic(C)
+        D = squareform(1.0 - C, checks=False)
+        Z = linkage(D, "average")
+        ref, _ = cophenet(Z, D)
+        assert abs(rho - ref) < 1e-12
+        assert np.allclose(np.sort(height), np.sort(Z[:, 2]), rtol=0, atol=1e-12)
+        assert sorted(order) == list(range(1, n + 1))
+        mem = cutree(merge, groups)
+        ref_mem = fcluster(Z, groups, criterion="maxclust")
+        # same partition up to relabelling
+        pairs = {(a, b) for a, b in zip(mem, ref_mem)}
+        assert len(pairs) == groups
+        assert mem[0] == 1
+
+
+def test_cutree_numbering():
+    from nmfconsensus_amd.nmf import cophenetic, cutree
+    C = np.array([[1, 1, 0, 0], [1, 1, 0, 0], [0, 0, 1, 1], [0, 0, 1, 1]], dtype=float)
+    rho, order, merge, height = cophenetic(C)
+    assert rho == pytest.approx(1.0)
+    assert list(cutree(merge, 2)) == [1, 1, 2, 2]
+    assert list(cutree(merge, 4)) == [1, 2, 3, 4]
+    assert list(cutree(merge, 1)) == [1, 1, 1, 1]

@@ -1,0 +1,79 @@
+"""The N>1 path on CPU: world_size-2 gloo ranks shard the C1 job grid and SUM-all-reduce their integer
+connectivity counts; the result equals the golden single-process counts bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, ret):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as dist
+    from nmfconsensus_amd.distributed import run_sharded_with
+    from pyoracle import Oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    z = np.load(os.path.join(ROOT, "tests", "golden", "golden.npz"), allow_pickle=False)
+    A = z["A_gct"]
+    ks = [int(k) for k in z["c1_ks"]]
+    R = int(z["c1_R"])
+    O = Oracle()
+
+    def runner(jb, je):
+        counts = np.zeros((len(ks), A.shape[1], A.shape[1]), dtype=np.int32)
+        for j in range(jb, je):
+            k = ks[j % len(ks)]
+            W0, H0 = O.init_restart(int(z["c1_seed"]) + j, A.shape[0], A.shape[1], k)
+            _, H, _ = O.nmf_mu(A, W0, H0, 10000, 1)
+            l = O.labels(H, 0)
+            counts[j % len(ks)] += (l[:, None] == l[None, :]).astype(np.int32)
+        return counts
+
+    out = run_sharded_with(runner, ks, R, A.shape[1], rank=rank, world=world)
+    if rank == 0:
+        ret.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_ranges_cover_jobs():
+    from nmfconsensus_amd.distributed import shard_range
+    for njobs in (1, 7, 80, 1800):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(njobs, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == njobs
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            sizes = [e - b for b, e in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_counts_equal_golden(golden):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = q.get(timeout=280)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i, k in enumerate(golden["c1_ks"]):
+        assert np.array_equal(out[i], golden[f"c1_counts_argmax_k{k}"])

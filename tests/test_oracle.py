@@ -1,0 +1,89 @@
+"""The oracle (our C restatement, oracle/nmf_oracle.c) pinned against the reference's golden vectors
+(tests/golden/golden.npz, produced by the reference's own C code) and against libc itself."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import relfro
+
+TOL = 1e-9
+
+
+def test_rand_stream_matches_libc_and_golden(golden, oracle):
+    libc = ctypes.CDLL(None)
+    libc.srand.argtypes = [ctypes.c_uint]
+    for s, draws in zip(golden["rand_seeds"], golden["rand_draws"]):
+        ours = oracle.rand_stream(int(s), draws.size)
+        assert np.array_equal(ours, draws), int(s)
+        libc.srand(int(s))
+        assert [libc.rand() for _ in range(50)] == list(draws[:50])
+
+
+def test_randnumber_values(golden, oracle):
+    # randnumber(0, 1) = rand() / (double)RAND_MAX (randnumber.c:34), bit-exact
+    W, H = oracle.init_restart(123, 64, 0, 1)
+    assert np.array_equal(W[:, 0], golden["randnumber_seed123"])
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 5])
+def test_init_bitexact(golden, oracle, k):
+    W, H = oracle.init_restart(123, 1000, 40, k)
+    assert np.array_equal(W, golden[f"init_k{k}_W"])
+    assert np.array_equal(H, golden[f"init_k{k}_H"])
+    W, H = oracle.init_restart(123, 5, 4, 2)
+    assert np.array_equal(W, golden["init_small_W"]) and np.array_equal(H, golden["init_small_H"])
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 5])
+def test_fixed_iterations(golden, oracle, k):
+    A = golden["A_gct"]
+    for T in (2, 10, 200, 398):
+        W, H, it = oracle.nmf_mu(A, golden[f"init_k{k}_W"], golden[f"init_k{k}_H"], T, 0)
+        assert it == T
+        assert relfro(W, golden[f"fixed_k{k}_T{T}_W"]) < TOL
+        assert relfro(H, golden[f"fixed_k{k}_T{T}_H"]) < TOL
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 5])
+def test_ref_compat_exit(golden, oracle, k):
+    A = golden["A_gct"]
+    W, H, it = oracle.nmf_mu(A, golden[f"init_k{k}_W"], golden[f"init_k{k}_H"], 10000, 1)
+    assert it == int(golden[f"refc_k{k}_iter"])
+    assert relfro(W, golden[f"refc_k{k}_W"]) < TOL
+    assert relfro(H, golden[f"refc_k{k}_H"]) < TOL
+
+
+def test_c1_sweep(golden, oracle):
+    """runNMFinJobs semantics (nmf.r:106-143) on the bundled gct: per-job seeds, exits, labels, counts."""
+    A = golden["A_gct"]
+    m, n = A.shape
+    iters, Lam, Lro = [], [], []
+    for jk, js in zip(golden["c1_job_k"], golden["c1_job_seed"]):
+        W0, H0 = oracle.init_restart(int(js), m, n, int(jk))
+        W, H, it = oracle.nmf_mu(A, W0, H0, 10000, 1)
+        iters.append(it)
+        Lam.append(oracle.labels(H, 0))
+        Lro.append(oracle.labels(H, 1))
+    assert np.array_equal(np.array(iters), golden["c1_iters"])
+    Lam, Lro = np.array(Lam), np.array(Lro)
+    assert np.array_equal(Lam, golden["c1_labels_argmax"])
+    assert np.array_equal(Lro, golden["c1_labels_rorder"])
+    jk = golden["c1_job_k"]
+    for k in golden["c1_ks"]:
+        assert np.array_equal(oracle.counts(Lam[jk == k]), golden[f"c1_counts_argmax_k{k}"])
+        assert np.array_equal(oracle.counts(Lro[jk == k]), golden[f"c1_counts_rorder_k{k}"])
+
+
+def test_norm_maxchange(golden, oracle):
+    v, d = oracle.calculate_norm(golden["norm_a"], golden["norm_w"], golden["norm_h"])
+    assert abs(v - float(golden["norm_value"])) < 1e-14
+    assert relfro(d, golden["norm_d"]) < 1e-14
+    v, m0 = oracle.calculate_maxchange(golden["maxchange_mat"], golden["maxchange_mat0"])
+    assert v == float(golden["maxchange_value"])
+    assert np.array_equal(m0, golden["maxchange_mat0_after"])
+
+
+def test_golden_labels_have_margin(golden):
+    # labels are only meaningful as a bit-exact target when no column is a near-tie
+    assert golden["c1_margin_argmax"].min() > 1e-6
