@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""bench.py -- NMF restarts/sec for the consensus k-sweep on MI355X (BASELINE.json metric).
+
+A step = one full consensus sweep: every (k, restart) job of the workload runs from its libnmf
+generateMatrix(ran) init through the MU iterations under the reference's stop rule (REF_COMPAT,
+maxiter 10000), then labels, integer connectivity counts (RCCL SUM all-reduce when N > 1),
+consensus = counts / R and the cophenetic correlation per k.  A is resident in HBM before timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  value = restarts completed by all ranks / max-over-ranks wall time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix peak (spec); probe measured ~70
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline: the reference's own nmf_mu (oracle/_ref, compiled from /root/reference sources) timed
+# on the host cores, one single-threaded-BLAS process per core (BatchJobs njobs semantics, nmf.r:111).
+# ------------------------------------------------------------------------------------------------
+def _cpu_worker(args):
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    m, n, ks, T, kind = args
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    from nmfconsensus_amd.synthetic import planted_matrix
+    import pyoracle
+
+    A = planted_matrix(m, n)
+    out = {}
+    if kind == "reference":
+        lib = pyoracle.RefLib()
+        for k in ks:
+            W0, H0 = lib.generate_ran(123 + k, m, n, k)
+            t0 = time.perf_counter()
+            lib.nmf_mu(A, W0, H0, T)
+            out[k] = (time.perf_counter() - t0) / T
+    else:
+        O = pyoracle.Oracle()
+        for k in ks:
+            W0, H0 = O.init_restart(123 + k, m, n, k)
+            t0 = time.perf_counter()
+            O.nmf_mu(A, W0, H0, T, 0)
+            out[k] = (time.perf_counter() - t0) / T
+    return out
+
+
+def cpu_baseline(m, n, ks, mean_iters_per_k, cores, T):
+    import multiprocessing as mp
+    import contextlib
+
+    kind = "reference" if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libnmf_ref.so")) else "port"
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    saved = os.dup(1)
+    os.dup2(devnull, 1)   # the reference prints "Exiting nmf_mu after ..." per call (nmf_mu.c:296)
+    try:
+        with ctx.Pool(cores) as pool:
+            res = pool.map(_cpu_worker, [(m, n, ks, T, kind)] * cores)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+        os.close(devnull)
+    wall = time.perf_counter() - t0
+    t_iter = {k: sum(r[k] for r in res) / len(res) for k in ks}
+    # sweep of R restarts per k on `cores` processes: CPU-seconds = R * sum_k t_iter(k) * I(k)
+    per_restart_set = sum(t_iter[k] * mean_iters_per_k[k] for k in ks)
+    value = len(ks) * cores / per_restart_set
+    with contextlib.suppress(Exception):
+        pass
+    return {
+        "value": value,
+        "unit": "restarts/s",
+        "cores": cores,
+        "kind": kind,
+        "sample": (f"{'reference libnmf nmf_mu (oracle/_ref, scipy OpenBLAS, 1 thread/process)' if kind == 'reference' else 'oracle C restatement'}"
+                   f" x {cores} concurrent processes, {T} iterations per k={ks[0]}..{ks[-1]} on the {m}x{n} matrix; "
+                   f"restarts/s extrapolated with the GPU run's mean iterations per k; sample wall {wall:.1f} s"),
+        "sec_per_iter": {str(k): t_iter[k] for k in ks},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4"])
+    ap.add_argument("--maxiter", type=int, default=10000)
+    ap.add_argument("--stop-rule", default="ref_compat", choices=["fixed", "ref_compat", "argmax_stable"])
+    ap.add_argument("--restarts", type=int, default=None, help="override R (restarts per k)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=10)
+    ap.add_argument("--cpu-cores", type=int, default=None)
+    ap.add_argument("--no-timing", action="store_true", help="disable per-launch HIP event timing")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from nmfconsensus_amd.synthetic import CONFIGS, planted_matrix
+    from nmfconsensus_amd.nmf import Engine, cophenetic
+    from nmfconsensus_amd.distributed import shard_range
+    from nmfconsensus_amd import _lib
+
+    m, n, ks, R, desc = CONFIGS[args.config]
+    if args.restarts:
+        R = args.restarts
+    nk = len(ks)
+    stop_rule = {"fixed": 0, "ref_compat": 1, "argmax_stable": 2}[args.stop_rule]
+
+    A_host = planted_matrix(m, n)
+    A_dev = torch.from_numpy(A_host.T.copy()).to(dev)          # (n, m) row-major == (m, n) column-major
+    torch.cuda.synchronize()
+    eng = Engine(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local)
+    counts = torch.zeros((nk, n, n), dtype=torch.int32, device=dev)
+    jb, je = shard_range(nk * R, rank, world)
+    timing = not args.no_timing
+
+    def step():
+        res = eng.run(ks, R, maxiter=args.maxiter, seed=123, stop_rule=stop_rule, job_begin=jb, job_end=je,
+                      counts_device_ptr=counts.data_ptr(), check_every=16)
+        if world > 1:
+            torch.distributed.all_reduce(counts, op=torch.distributed.ReduceOp.SUM)
+        cons = counts.to(torch.float64) / R
+        rho = {}
+        if rank == 0:
+            C = cons.cpu().numpy()
+            for i, k in enumerate(ks):
+                rho[k] = cophenetic(C[i])[0]
+        return res, rho
+
+    eng.set_timing(False)
+    for _ in range(args.warmup):
+        step()
+    eng.set_timing(timing)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iters_all, wta = [], [0, 0.0, 0.0]
+    ahtw = [0, 0.0, 0.0]
+    hupd = [0, 0.0]
+    last = None
+    for _ in range(args.steps):
+        res, rho = step()
+        last = (res, rho)
+        iters_all.append(res.iters.copy())
+        for acc, kid in ((wta, _lib.KID_WTA), (ahtw, _lib.KID_AHTW)):
+            c, ms = eng.kernel_time(kid)
+            acc[0] += c
+            acc[1] += ms
+            acc[2] += eng.kernel_flops(kid) * c
+        c, ms = eng.kernel_time(_lib.KID_HUPD)
+        hupd[0] += c
+        hupd[1] += ms
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    res, rho = last
+    total_restarts = nk * R * args.steps
+    value = total_restarts / elapsed
+    its = np.concatenate(iters_all)
+    local_jobs = np.arange(jb, je)
+    mean_iter_k = {k: float(np.mean(res.iters[(local_jobs % nk) == i])) for i, k in enumerate(ks)}
+    log(f"[bench] rank {rank}: {je - jb} restarts/step, mean iters {its.mean():.1f} (max {its.max()}), "
+        f"step {elapsed / args.steps:.3f} s, engine {res.seconds_total:.3f} s (iterate {res.seconds_iterate:.3f} s)")
+
+    roof = None
+    kernels = {}
+    if timing and wta[0] and ahtw[0]:
+        for name, acc in (("wta", wta), ("ahtw", ahtw)):
+            avg_ms = acc[1] / acc[0]
+            fl = acc[2] / acc[0]
+            kernels[name] = {"launches": acc[0], "avg_ms": avg_ms, "algo_flop_per_launch": fl,
+                             "tflops": fl / (avg_ms * 1e-3) / 1e12}
+        kernels["hupdate"] = {"launches": hupd[0], "avg_ms": hupd[1] / max(hupd[0], 1)}
+        dom = max(("wta", "ahtw"), key=lambda s: kernels[s]["avg_ms"] * kernels[s]["launches"])
+        ach = kernels[dom]["tflops"]
+        roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None, "kernels": kernels}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        try:
+            cpu = cpu_baseline(m, n, ks, mean_iter_k, cores, args.cpu_iters)
+        except Exception as ex:  # reported, never fatal for the GPU number
+            log(f"[bench] cpu baseline failed: {ex!r}")
+
+    if rank == 0:
+        out = {
+            "metric": "NMF restarts/sec (k=2..10 sweep, 20k×500 fp64) + fp64-MFMA/HBM roofline %",
+            "value": value,
+            "unit": "restarts/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (planted 4-group matrix, splitmix64 seed 20261015; per-job generateMatrix(ran) init)",
+            "config": {"workload": f"{args.config}: {desc}, stop rule {args.stop_rule}, maxiter {args.maxiter}",
+                       "m": m, "n": n, "ks": ks, "restarts_per_k": R, "jobs": nk * R,
+                       "parallelism": f"jobs sharded over {world} GPU(s), RCCL int32 all-reduce of counts",
+                       "mean_iterations": float(its.mean()), "max_iterations": int(its.max()),
+                       "cophenetic_rho": {str(k): v for k, v in rho.items()}},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

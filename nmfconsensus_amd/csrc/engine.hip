@@ -4,9 +4,10 @@
 // (libnmf/nmf_mu.c:167-293) and the consensus reduction (nmf.r:121-144) with one batched sweep on
 // one MI355X: all (k, restart) jobs of a shard are packed into 64-column panels of a stacked W/H,
 // and every MU iteration is three launches on one HIP stream:
-//   k_wta     G = W^T A and the panel Grams W^T W            (fp64 MFMA, split over fixed gene chunks)
-//   k_hupdate H update, H H^T, stability check per restart   (one workgroup per restart)
-//   k_ahtw    A H^T fused with W0 (H H^T) and the W update   (fp64 MFMA, epilogue in LDS)
+//   k_wta     G = W^T A                                          (fp64 MFMA, fixed gene chunks)
+//   k_hupdate W^T W from Gram partials, H update, H H^T, stability check (one workgroup per restart)
+//   k_ahtw    A h^T fused with W0 (h h^T), the W update and the next Gram partials (fp64 MFMA)
+// Restarts that stop are archived and the live ones repacked into fewer panels as the sweep goes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -15,7 +16,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <string>
 #include <vector>
 
@@ -89,14 +89,13 @@ void mat_mul31(const uint32_t* A, const uint32_t* B, uint32_t* C) {
 }
 
 std::vector<uint32_t> make_jump_table(int nchunks) {
-  std::vector<uint32_t> M(31 * 31, 0), P(31 * 31, 0), T(31 * 31), R(31 * 31);
+  std::vector<uint32_t> M(31 * 31, 0), P(31 * 31, 0), T(31 * 31);
   for (int q = 0; q < 30; ++q) M[q * 31 + q + 1] = 1;
-  M[30 * 31 + 0] = 1;   // r[i-31]
-  M[30 * 31 + 28] += 1; // r[i-3]
-  // P = M^RCHUNK by repeated squaring
+  M[30 * 31 + 0] = 1;    // r[i-31]
+  M[30 * 31 + 28] += 1;  // r[i-3]
   for (int i = 0; i < 31; ++i) P[i * 31 + i] = 1;
   std::vector<uint32_t> base = M;
-  for (int e = RCHUNK; e > 0; e >>= 1) {
+  for (int e = RCHUNK; e > 0; e >>= 1) {   // P = M^RCHUNK
     if (e & 1) {
       mat_mul31(P.data(), base.data(), T.data());
       P = T;
@@ -106,13 +105,49 @@ std::vector<uint32_t> make_jump_table(int nchunks) {
   }
   std::vector<uint32_t> table((size_t)std::max(nchunks, 1) * 961, 0);
   for (int i = 0; i < 31; ++i) table[i * 31 + i] = 1;
-  for (int c = 1; c < nchunks; ++c) {
-    mat_mul31(P.data(), &table[(size_t)(c - 1) * 961], &table[(size_t)c * 961]);
-  }
+  for (int c = 1; c < nchunks; ++c) mat_mul31(P.data(), &table[(size_t)(c - 1) * 961], &table[(size_t)c * 961]);
   return table;
 }
 
-enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_LABEL = 4, KID_N = 5 };
+enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID_N = 5 };
+
+// Packing of a restart list into 64-column panels (sequential fill, k-descending order given);
+// panel count rounded up to an even number (the W^T A tile spans a panel pair).
+struct Packing {
+  std::vector<RestartInfo> ri;   // active list, panel-contiguous
+  std::vector<int> prb, pre;     // per panel: [begin, end) in ri
+  int npanels = 0;
+};
+
+Packing pack(const std::vector<RestartInfo>& in) {
+  Packing pk;
+  int fill = PANEL, np = -1;
+  for (size_t q = 0; q < in.size(); ++q) {
+    RestartInfo r = in[q];
+    if (fill + r.k > PANEL) {
+      ++np;
+      fill = 0;
+      pk.prb.push_back((int)q);
+      pk.pre.push_back((int)q);
+    }
+    r.col0 = np * PANEL + fill;
+    fill += r.k;
+    pk.ri.push_back(r);
+    pk.pre[np] = (int)q + 1;
+  }
+  pk.npanels = np + 1;
+  if (pk.npanels & 1) {   // empty partner panel
+    pk.prb.push_back((int)in.size());
+    pk.pre.push_back((int)in.size());
+    ++pk.npanels;
+  }
+  if (pk.npanels == 0) {
+    pk.npanels = 2;
+    pk.prb = {0, 0};
+    pk.pre = {0, 0};
+  }
+  return pk;
+}
 
 }  // namespace
 
@@ -121,12 +156,12 @@ struct nmfc_engine {
   hipStream_t st = nullptr;
   int m = 0, n = 0;
   long m_pad = 0, n_pad = 0, n_cols_pad = 0;
-  int kchunk = 0, nsplit = 0;
+  int kchunk = 0, nsplit = 0, ngt = 0;
   DevBuf Acm, Arm;
   // per-run buffers (grow-only)
-  DevBuf W, H, Gpart, SWpart, SHp;
+  DevBuf W[2], H[2], Gpart, SWpart, SH, Hfin, Wfin;
   DevBuf rinfo, stop_iter, stop_reason, unchanged, classes, n_stopped;
-  DevBuf prb, pre, pcs, pck, pcr;
+  DevBuf prb, pre, moves, finfo;
   DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp;
   int jump_chunks = 0;
   int* h_stopped = nullptr;   // pinned, 2 slots
@@ -141,6 +176,7 @@ struct nmfc_engine {
   double kms[KID_N] = {0};
   long long kcount[KID_N] = {0};
   double kflops[KID_N] = {0};
+  int repacks = 0;
 };
 
 namespace {
@@ -169,6 +205,7 @@ void drain_timing(nmfc_engine* e) {
   e->pending.clear();
 }
 
+// HIP events on the engine's stream around one launch (only when timing is enabled)
 struct TimedLaunch {
   nmfc_engine* e;
   int kid;
@@ -197,7 +234,7 @@ struct TimedLaunch {
 extern "C" {
 
 const char* nmfc_last_error(void) { return g_err.c_str(); }
-const char* nmfc_version(void) { return "nmfconsensus_amd 0.1 (gfx950, fp64 MFMA)"; }
+const char* nmfc_version(void) { return "nmfconsensus_amd 0.2 (gfx950, fp64 MFMA)"; }
 
 void nmfc_default_opts(nmfc_sweep_opts* o) {
   memset(o, 0, sizeof *o);
@@ -233,10 +270,11 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if ((err = hipHostMalloc((void**)&e->h_stopped, 2 * sizeof(int), 0)) != hipSuccess) return fail("hipHostMalloc", err);
   e->m = m;
   e->n = n;
-  e->m_pad = round_up(m, TILE);
-  e->n_pad = round_up(n, BK);
-  e->n_cols_pad = round_up(n, TILE);
-  // fixed gene chunks: a function of m only, so every entry's reduction order is batch-independent
+  e->m_pad = round_up(m, GT);          // gene tiles of A h^T and Gram partials
+  e->n_pad = round_up(n, BK);          // K of A h^T
+  e->n_cols_pad = round_up(n, 128);    // sample tiles of W^T A
+  e->ngt = (int)(e->m_pad / GT);
+  // fixed gene chunks of W^T A: a function of m only, so every entry's summation order is batch-independent
   e->kchunk = 4096;
   e->nsplit = (int)((e->m_pad + e->kchunk - 1) / e->kchunk);
   if (e->Acm.ensure(sizeof(double) * e->n_cols_pad * e->m_pad) || e->Arm.ensure(sizeof(double) * e->m_pad * e->n_pad)) {
@@ -270,10 +308,12 @@ void nmfc_engine_destroy(nmfc_engine* e) {
   if (e->st) (void)hipStreamSynchronize(e->st);
   drain_timing(e);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
-  DevBuf* bufs[] = {&e->Acm, &e->Arm, &e->W, &e->H, &e->Gpart, &e->SWpart, &e->SHp, &e->rinfo, &e->stop_iter,
-                    &e->stop_reason, &e->unchanged, &e->classes, &e->n_stopped, &e->prb, &e->pre, &e->pcs, &e->pck,
-                    &e->pcr, &e->initjobs, &e->chunk_job, &e->chunk_idx, &e->jump, &e->labels, &e->slot,
-                    &e->grp_begin, &e->grp_list, &e->counts_tmp, &e->cons_tmp};
+  DevBuf* bufs[] = {&e->Acm,       &e->Arm,       &e->W[0],      &e->W[1],     &e->H[0],       &e->H[1],
+                    &e->Gpart,     &e->SWpart,    &e->SH,        &e->Hfin,     &e->Wfin,       &e->rinfo,
+                    &e->stop_iter, &e->stop_reason, &e->unchanged, &e->classes, &e->n_stopped, &e->prb,
+                    &e->pre,       &e->moves,     &e->finfo,     &e->initjobs, &e->chunk_job,  &e->chunk_idx,
+                    &e->jump,      &e->labels,    &e->slot,      &e->grp_begin, &e->grp_list,  &e->counts_tmp,
+                    &e->cons_tmp};
   for (DevBuf* b : bufs) b->release();
   if (e->h_stopped) (void)hipHostFree(e->h_stopped);
   if (e->st) (void)hipStreamDestroy(e->st);
@@ -309,7 +349,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   if (opts.check_every <= 0) opts.check_every = 16;
   const int m = e->m, n = e->n;
   for (int q = 0; q < nk; ++q) {
-    // nmf.r:107-108 rejects k = 1; the LDS arrays of k_hupdate hold k <= KMAX.
+    // nmf.r:107-108 rejects k = 1; the per-restart LDS blocks hold k <= KMAX.
     if (ks[q] < 2 || ks[q] > KMAX || ks[q] > n || ks[q] > m) {
       set_err("nmfc_engine_run: k=%d unsupported (need 2 <= k <= min(%d, m, n))", ks[q], KMAX);
       return -1;
@@ -330,6 +370,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     e->kcount[q] = 0;
     e->kflops[q] = 0;
   }
+  e->repacks = 0;
   const long njobs_all = (long)nk * R;
   const long jb = std::max(0, opts.job_begin);
   const long je = (opts.job_end < 0) ? njobs_all : std::min<long>(opts.job_end, njobs_all);
@@ -338,93 +379,86 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     return -1;
   }
   const int nj = (int)(je - jb);
+  auto job_k = [&](int s) { return ks[(jb + s) % nk]; };
 
-  // ---- packing: restarts grouped by k (descending), sequential fill of 64-column panels ----
+  // ---- restart ids: shard jobs in k-descending order (packing order) ----
   std::vector<int> order(nj);
   for (int i = 0; i < nj; ++i) order[i] = i;
-  auto job_k = [&](int s) { return ks[(jb + s) % nk]; };
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return job_k(a) > job_k(b); });
-  std::vector<RestartInfo> ri(nj);
-  std::vector<int> rslot(nj);                 // restart index -> shard job slot
-  std::vector<int> prb_h, pre_h;
-  int fill = TILE, np = -1;
-  for (int q = 0; q < nj; ++q) {
-    const int s = order[q];
-    const int k = job_k(s);
-    if (fill + k > TILE) {
-      ++np;
-      fill = 0;
-      prb_h.push_back(q);
-      pre_h.push_back(q);
-    }
-    ri[q].col0 = np * TILE + fill;
-    ri[q].k = k;
-    rslot[q] = s;
-    fill += k;
-    pre_h[np] = q + 1;
+  std::vector<RestartInfo> all(nj);
+  std::vector<int> rslot(nj);          // rid -> shard job slot
+  std::vector<int> hoff(nj + 1, 0);    // rid -> first archive row
+  long sw_total = 0;
+  for (int rid = 0; rid < nj; ++rid) {
+    const int s = order[rid];
+    all[rid].k = job_k(s);
+    all[rid].rid = rid;
+    all[rid].sq_off = (int)sw_total;
+    all[rid].col0 = 0;
+    rslot[rid] = s;
+    sw_total += (long)all[rid].k * all[rid].k;
+    hoff[rid + 1] = hoff[rid] + all[rid].k;
   }
-  const int npanels = np + 1;
-  const long Kt_pad = (long)npanels * TILE;
-  std::vector<int> pcs_h(Kt_pad, -1), pck_h(Kt_pad, 0), pcr_h(Kt_pad, -1);
-  for (int q = 0; q < nj; ++q) {
-    const int p = ri[q].col0 / TILE, lc = ri[q].col0 % TILE;
-    for (int a = 0; a < ri[q].k; ++a) {
-      pcs_h[(long)p * TILE + lc + a] = lc;
-      pck_h[(long)p * TILE + lc + a] = ri[q].k;
-      pcr_h[(long)p * TILE + lc + a] = q;
-    }
-  }
-  const int ntj = (int)(e->n_cols_pad / TILE);
-  const int ngt = (int)(e->m_pad / TILE);
+  Packing pk = pack(all);
+  const long cap_cols = (long)pk.npanels * PANEL;
+  const int ntj = (int)(e->n_cols_pad / 128);
   const long g_ld = e->n_cols_pad;
-  const long g_split = Kt_pad * g_ld;
-  const long sw_split = (long)npanels * TILE * TILE;
+  const long g_split = cap_cols * g_ld;
   const long cls_ld = std::max<long>(n, KMAX);
+  const long fin_rows = hoff[nj];
+  const bool want_w = out && out->W;
 
   // ---- device buffers ----
-  if (e->W.ensure(sizeof(double) * Kt_pad * e->m_pad) || e->H.ensure(sizeof(double) * Kt_pad * e->n_pad) ||
-      e->Gpart.ensure(sizeof(double) * g_split * e->nsplit) || e->SWpart.ensure(sizeof(double) * sw_split * e->nsplit) ||
-      e->SHp.ensure(sizeof(double) * sw_split) || e->rinfo.ensure(sizeof(RestartInfo) * nj) ||
-      e->stop_iter.ensure(sizeof(int) * nj) || e->stop_reason.ensure(sizeof(int) * nj) ||
-      e->unchanged.ensure(sizeof(int) * nj) || e->classes.ensure(sizeof(int) * nj * cls_ld) ||
-      e->n_stopped.ensure(sizeof(int)) || e->prb.ensure(sizeof(int) * npanels) || e->pre.ensure(sizeof(int) * npanels) ||
-      e->pcs.ensure(sizeof(int) * Kt_pad) || e->pck.ensure(sizeof(int) * Kt_pad) || e->pcr.ensure(sizeof(int) * Kt_pad) ||
-      e->labels.ensure(sizeof(int32_t) * (size_t)nj * n) || e->slot.ensure(sizeof(int) * nj))
+  if (e->W[0].ensure(sizeof(double) * cap_cols * e->m_pad) || e->H[0].ensure(sizeof(double) * cap_cols * e->n_pad) ||
+      e->W[1].ensure(sizeof(double) * cap_cols * e->m_pad) || e->H[1].ensure(sizeof(double) * cap_cols * e->n_pad) ||
+      e->Gpart.ensure(sizeof(double) * g_split * e->nsplit) || e->SWpart.ensure(sizeof(double) * sw_total * e->ngt) ||
+      e->SH.ensure(sizeof(double) * sw_total) || e->Hfin.ensure(sizeof(double) * fin_rows * e->n_pad) ||
+      (want_w && e->Wfin.ensure(sizeof(double) * fin_rows * e->m_pad)) || e->rinfo.ensure(sizeof(RestartInfo) * nj) ||
+      e->finfo.ensure(sizeof(RestartInfo) * nj) || e->stop_iter.ensure(sizeof(int) * nj) ||
+      e->stop_reason.ensure(sizeof(int) * nj) || e->unchanged.ensure(sizeof(int) * nj) ||
+      e->classes.ensure(sizeof(int) * nj * cls_ld) || e->n_stopped.ensure(sizeof(int)) ||
+      e->prb.ensure(sizeof(int) * pk.npanels) || e->pre.ensure(sizeof(int) * pk.npanels) ||
+      e->moves.ensure(sizeof(MoveJob) * nj) || e->labels.ensure(sizeof(int32_t) * (size_t)nj * n) ||
+      e->slot.ensure(sizeof(int) * nj))
     return -1;
   hipStream_t st = e->st;
-  HCHECK(hipMemcpyAsync(e->rinfo.p, ri.data(), sizeof(RestartInfo) * nj, hipMemcpyHostToDevice, st));
-  HCHECK(hipMemcpyAsync(e->prb.p, prb_h.data(), sizeof(int) * npanels, hipMemcpyHostToDevice, st));
-  HCHECK(hipMemcpyAsync(e->pre.p, pre_h.data(), sizeof(int) * npanels, hipMemcpyHostToDevice, st));
-  HCHECK(hipMemcpyAsync(e->pcs.p, pcs_h.data(), sizeof(int) * Kt_pad, hipMemcpyHostToDevice, st));
-  HCHECK(hipMemcpyAsync(e->pck.p, pck_h.data(), sizeof(int) * Kt_pad, hipMemcpyHostToDevice, st));
-  HCHECK(hipMemcpyAsync(e->pcr.p, pcr_h.data(), sizeof(int) * Kt_pad, hipMemcpyHostToDevice, st));
+  int cur = 0;
+  auto upload_packing = [&](const Packing& p) -> int {
+    HCHECK(hipMemcpyAsync(e->rinfo.p, p.ri.data(), sizeof(RestartInfo) * std::max<size_t>(p.ri.size(), 1),
+                          hipMemcpyHostToDevice, st));
+    HCHECK(hipMemcpyAsync(e->prb.p, p.prb.data(), sizeof(int) * p.npanels, hipMemcpyHostToDevice, st));
+    HCHECK(hipMemcpyAsync(e->pre.p, p.pre.data(), sizeof(int) * p.npanels, hipMemcpyHostToDevice, st));
+    return 0;
+  };
+  if (upload_packing(pk)) return -1;
   HCHECK(hipMemcpyAsync(e->slot.p, rslot.data(), sizeof(int) * nj, hipMemcpyHostToDevice, st));
   HCHECK(hipMemsetAsync(e->stop_iter.p, 0, sizeof(int) * nj, st));
   HCHECK(hipMemsetAsync(e->stop_reason.p, 0, sizeof(int) * nj, st));
   HCHECK(hipMemsetAsync(e->unchanged.p, 0, sizeof(int) * nj, st));
   HCHECK(hipMemsetAsync(e->classes.p, 0, sizeof(int) * nj * cls_ld, st));   // nmf_mu.c:132 zero start
   HCHECK(hipMemsetAsync(e->n_stopped.p, 0, sizeof(int), st));
-  HCHECK(hipMemsetAsync(e->W.p, 0, sizeof(double) * Kt_pad * e->m_pad, st));
-  HCHECK(hipMemsetAsync(e->H.p, 0, sizeof(double) * Kt_pad * e->n_pad, st));
-  HCHECK(hipMemsetAsync(e->SHp.p, 0, sizeof(double) * sw_split, st));
+  HCHECK(hipMemsetAsync(e->W[0].p, 0, sizeof(double) * cap_cols * e->m_pad, st));
+  HCHECK(hipMemsetAsync(e->H[0].p, 0, sizeof(double) * cap_cols * e->n_pad, st));
+  HCHECK(hipMemsetAsync(e->W[1].p, 0, sizeof(double) * cap_cols * e->m_pad, st));
+  HCHECK(hipMemsetAsync(e->H[1].p, 0, sizeof(double) * cap_cols * e->n_pad, st));
 
   // ---- init ----
   if (W_init && H_init) {
     // caller-provided factors, shard-job-major: W_j (m x k), H_j (k x n)
-    std::vector<long> woff(nj + 1, 0), hoff(nj + 1, 0);
+    std::vector<long> woff(nj + 1, 0), ho(nj + 1, 0);
     for (int s = 0; s < nj; ++s) {
       woff[s + 1] = woff[s] + (long)m * job_k(s);
-      hoff[s + 1] = hoff[s] + (long)job_k(s) * n;
+      ho[s + 1] = ho[s] + (long)job_k(s) * n;
     }
     std::vector<double> hrow;
-    for (int q = 0; q < nj; ++q) {
-      const int s = rslot[q], k = ri[q].k;
-      HCHECK(hipMemcpy2DAsync(e->W.as<double>() + (long)ri[q].col0 * e->m_pad, sizeof(double) * e->m_pad,
+    for (const RestartInfo& r : pk.ri) {
+      const int s = rslot[r.rid], k = r.k;
+      HCHECK(hipMemcpy2DAsync(e->W[0].as<double>() + (long)r.col0 * e->m_pad, sizeof(double) * e->m_pad,
                               W_init + woff[s], sizeof(double) * m, sizeof(double) * m, k, hipMemcpyHostToDevice, st));
       hrow.assign((size_t)k * n, 0.0);
       for (int j = 0; j < n; ++j)
-        for (int a = 0; a < k; ++a) hrow[(size_t)a * n + j] = H_init[hoff[s] + (long)j * k + a];
-      HCHECK(hipMemcpy2DAsync(e->H.as<double>() + (long)ri[q].col0 * e->n_pad, sizeof(double) * e->n_pad, hrow.data(),
+        for (int a = 0; a < k; ++a) hrow[(size_t)a * n + j] = H_init[ho[s] + (long)j * k + a];
+      HCHECK(hipMemcpy2DAsync(e->H[0].as<double>() + (long)r.col0 * e->n_pad, sizeof(double) * e->n_pad, hrow.data(),
                               sizeof(double) * n, sizeof(double) * n, k, hipMemcpyHostToDevice, st));
       HCHECK(hipStreamSynchronize(st));   // hrow is reused
     }
@@ -433,12 +467,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     std::vector<int> cj, ci;
     int maxch = 1;
     for (int q = 0; q < nj; ++q) {
-      const int s = rslot[q];
-      const long total = (long)m * ri[q].k + (long)ri[q].k * n;
+      const RestartInfo& r = pk.ri[q];
+      const long total = (long)m * r.k + (long)r.k * n;
       const int nch = (int)((total + RCHUNK - 1) / RCHUNK);
-      ij[q].seed = (uint32_t)(opts.seed + (uint32_t)(jb + s));   // job seed = seed + job_id - 1
-      ij[q].col0 = ri[q].col0;
-      ij[q].k = ri[q].k;
+      ij[q].seed = (uint32_t)(opts.seed + (uint32_t)(jb + rslot[r.rid]));   // job seed = seed + job_id - 1
+      ij[q].col0 = r.col0;
+      ij[q].k = r.k;
       ij[q].nchunks = nch;
       maxch = std::max(maxch, nch);
       for (int c = 0; c < nch; ++c) {
@@ -464,46 +498,78 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       TimedLaunch tl(e, KID_INIT);
       hipLaunchKernelGGL(k_init, dim3((total_chunks + NT - 1) / NT), dim3(NT), 0, st, e->initjobs.as<InitJob>(),
                          e->chunk_job.as<int>(), e->chunk_idx.as<int>(), total_chunks, e->jump.as<uint32_t>(), m, n,
-                         e->m_pad, e->n_pad, opts.min_init, opts.max_init, e->W.as<double>(), e->H.as<double>());
+                         e->m_pad, e->n_pad, opts.min_init, opts.max_init, e->W[0].as<double>(), e->H[0].as<double>());
     }
     HCHECK(hipGetLastError());
     HCHECK(hipStreamSynchronize(st));   // host vectors cj/ci go out of scope
   }
+  // Gram partials of W0 for iteration 1
+  {
+    TimedLaunch tl(e, KID_INIT);
+    hipLaunchKernelGGL(k_gram, dim3(pk.npanels * e->ngt), dim3(NT), 0, st, e->W[0].as<double>(), e->m_pad, pk.npanels,
+                       e->ngt, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->stop_iter.as<int>(),
+                       e->SWpart.as<double>(), sw_total);
+  }
+  HCHECK(hipGetLastError());
+
+  // archive rows of restarts (final H, and W when requested) from the current buffers
+  std::vector<char> archived(nj, 0);
+  auto archive = [&](const std::vector<RestartInfo>& list) -> int {
+    if (list.empty()) return 0;
+    std::vector<MoveJob> mv(list.size());
+    for (size_t q = 0; q < list.size(); ++q) mv[q] = {list[q].col0, hoff[list[q].rid], list[q].k};
+    HCHECK(hipMemcpyAsync(e->moves.p, mv.data(), sizeof(MoveJob) * mv.size(), hipMemcpyHostToDevice, st));
+    {
+      TimedLaunch tl(e, KID_OTHER);
+      hipLaunchKernelGGL(k_move_rows, dim3((unsigned)mv.size(), 2), dim3(NT), 0, st, e->moves.as<MoveJob>(),
+                         e->H[cur].as<double>(), e->n_pad, e->Hfin.as<double>(), e->n_pad, e->n_pad);
+      if (want_w)
+        hipLaunchKernelGGL(k_move_rows, dim3((unsigned)mv.size(), 16), dim3(NT), 0, st, e->moves.as<MoveJob>(),
+                           e->W[cur].as<double>(), e->m_pad, e->Wfin.as<double>(), e->m_pad, e->m_pad);
+    }
+    HCHECK(hipGetLastError());
+    HCHECK(hipStreamSynchronize(st));   // mv is a host temporary
+    for (const RestartInfo& r : list) archived[r.rid] = 1;
+    return 0;
+  };
 
   // ---- iterate ----
   auto t_iter0 = std::chrono::steady_clock::now();
-  const int grid_wta = e->nsplit * npanels * (ntj + 1);
-  const int grid_ahtw = npanels * ngt;
   int it = 0, q = 0, checked = 0;
-  int iters_done = 0;
+  int nact = nj;
+  int stopped_at_pack = 0;
   hipEvent_t ev[2];
   HCHECK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
   HCHECK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  std::vector<int> si(nj);
   for (;;) {
     if (it < opts.maxiter) {
       const int chunk = std::min(opts.check_every, opts.maxiter - it);
+      const int npairs = pk.npanels / 2;
+      const int grid_wta = e->nsplit * npairs * ntj;
+      const int grid_ahtw = pk.npanels * e->ngt;
       for (int c = 1; c <= chunk; ++c) {
         const int iter = it + c;
         {
           TimedLaunch tl(e, KID_WTA);
-          hipLaunchKernelGGL(k_wta, dim3(grid_wta), dim3(NT), 0, st, e->W.as<double>(), e->Acm.as<double>(), e->m_pad,
-                             npanels, ntj, e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->stop_iter.as<int>(), iter,
-                             e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_split);
+          hipLaunchKernelGGL(k_wta, dim3(grid_wta), dim3(NT), 0, st, e->W[cur].as<double>(), e->Acm.as<double>(),
+                             e->m_pad, npairs, ntj, e->nsplit, e->kchunk, e->prb.as<int>(), e->pre.as<int>(),
+                             e->rinfo.as<RestartInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split);
         }
         {
           TimedLaunch tl(e, KID_HUPD);
-          hipLaunchKernelGGL(k_hupdate, dim3(nj), dim3(NT), 0, st, iter, opts.maxiter, opts.stop_rule,
+          hipLaunchKernelGGL(k_hupdate, dim3(nact), dim3(NT), 0, st, iter, opts.maxiter, opts.stop_rule,
                              e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, e->nsplit,
-                             e->SWpart.as<double>(), sw_split, e->H.as<double>(), e->SHp.as<double>(),
+                             e->SWpart.as<double>(), sw_total, e->ngt, e->H[cur].as<double>(), e->SH.as<double>(),
                              e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->unchanged.as<int>(),
                              e->classes.as<int>(), cls_ld, e->n_stopped.as<int>());
         }
         {
           TimedLaunch tl(e, KID_AHTW);
-          hipLaunchKernelGGL(k_ahtw, dim3(grid_ahtw), dim3(NT), 0, st, iter, e->H.as<double>(), e->n_pad,
-                             e->Arm.as<double>(), e->m_pad, e->W.as<double>(), e->SHp.as<double>(), e->pcs.as<int>(),
-                             e->pck.as<int>(), e->pcr.as<int>(), e->prb.as<int>(), e->pre.as<int>(),
-                             e->stop_iter.as<int>(), ngt);
+          hipLaunchKernelGGL(k_ahtw, dim3(grid_ahtw), dim3(NT), 0, st, iter, e->H[cur].as<double>(), e->n_pad,
+                             e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(), e->SH.as<double>(),
+                             e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->stop_iter.as<int>(),
+                             pk.npanels, e->ngt, e->SWpart.as<double>(), sw_total);
         }
       }
       HCHECK(hipGetLastError());
@@ -515,25 +581,69 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     // consume polls, keeping one chunk in flight while there is more to enqueue
     const int target = (it < opts.maxiter) ? q - 1 : q;
     bool done = false;
+    int stopped = 0;
     while (checked < target) {
       HCHECK(hipEventSynchronize(ev[checked & 1]));
-      if (e->h_stopped[checked & 1] >= nj) done = true;
+      stopped = e->h_stopped[checked & 1];
+      if (stopped >= nj) done = true;
       ++checked;
     }
     if (e->timing) drain_timing(e);
     if (done || (it >= opts.maxiter && checked == q)) break;
+    // repack when a fifth of the live restarts have stopped since the last packing
+    if (stopped - stopped_at_pack >= std::max(1, nact / 5)) {
+      HCHECK(hipStreamSynchronize(st));
+      if (e->timing) drain_timing(e);
+      checked = q;   // every poll is now complete
+      HCHECK(hipMemcpy(si.data(), e->stop_iter.p, sizeof(int) * nj, hipMemcpyDeviceToHost));
+      std::vector<RestartInfo> gone, live;
+      for (const RestartInfo& r : pk.ri) (si[r.rid] ? gone : live).push_back(r);
+      if (archive(gone)) return -1;
+      Packing np = pack(live);
+      std::vector<MoveJob> mv(np.ri.size());
+      for (size_t x = 0; x < np.ri.size(); ++x) mv[x] = {live[x].col0, np.ri[x].col0, np.ri[x].k};
+      if (!mv.empty()) {
+        HCHECK(hipMemcpyAsync(e->moves.p, mv.data(), sizeof(MoveJob) * mv.size(), hipMemcpyHostToDevice, st));
+        {
+          TimedLaunch tl(e, KID_OTHER);
+          hipLaunchKernelGGL(k_move_rows, dim3((unsigned)mv.size(), 16), dim3(NT), 0, st, e->moves.as<MoveJob>(),
+                             e->W[cur].as<double>(), e->m_pad, e->W[cur ^ 1].as<double>(), e->m_pad, e->m_pad);
+          hipLaunchKernelGGL(k_move_rows, dim3((unsigned)mv.size(), 2), dim3(NT), 0, st, e->moves.as<MoveJob>(),
+                             e->H[cur].as<double>(), e->n_pad, e->H[cur ^ 1].as<double>(), e->n_pad, e->n_pad);
+        }
+        HCHECK(hipGetLastError());
+      }
+      cur ^= 1;
+      pk = np;
+      if (upload_packing(pk)) return -1;
+      HCHECK(hipStreamSynchronize(st));   // mv / pk host data uploaded
+      nact = (int)pk.ri.size();
+      stopped_at_pack = nj - nact;
+      ++e->repacks;
+      if (nact == 0) break;
+    }
   }
   HCHECK(hipStreamSynchronize(st));
+  if (e->timing) drain_timing(e);
   (void)hipEventDestroy(ev[0]);
   (void)hipEventDestroy(ev[1]);
-  iters_done = it;
+  const int iters_enqueued = it;
   auto t_iter1 = std::chrono::steady_clock::now();
-
-  // ---- labels, counts ----
   {
-    TimedLaunch tl(e, KID_LABEL);
-    hipLaunchKernelGGL(k_labels, dim3((n + NT - 1) / NT, nj), dim3(NT), 0, st, e->rinfo.as<RestartInfo>(),
-                       e->slot.as<int>(), e->H.as<double>(), e->n_pad, n, opts.label_rule, e->labels.as<int32_t>());
+    std::vector<RestartInfo> rest;
+    for (const RestartInfo& r : pk.ri)
+      if (!archived[r.rid]) rest.push_back(r);
+    if (archive(rest)) return -1;
+  }
+
+  // ---- labels, counts (from the archive) ----
+  std::vector<RestartInfo> fin(nj);
+  for (int rid = 0; rid < nj; ++rid) fin[rid] = {hoff[rid], all[rid].k, rid, all[rid].sq_off};
+  HCHECK(hipMemcpyAsync(e->finfo.p, fin.data(), sizeof(RestartInfo) * nj, hipMemcpyHostToDevice, st));
+  {
+    TimedLaunch tl(e, KID_OTHER);
+    hipLaunchKernelGGL(k_labels, dim3((n + NT - 1) / NT, nj), dim3(NT), 0, st, e->finfo.as<RestartInfo>(),
+                       e->slot.as<int>(), e->Hfin.as<double>(), e->n_pad, n, opts.label_rule, e->labels.as<int32_t>());
   }
   HCHECK(hipGetLastError());
   std::vector<int> gb(nk + 1, 0), gl;
@@ -557,7 +667,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       dcounts = e->counts_tmp.as<int32_t>();
     }
     {
-      TimedLaunch tl(e, KID_LABEL);
+      TimedLaunch tl(e, KID_OTHER);
       hipLaunchKernelGGL(k_counts, dim3((n + 15) / 16, (n + 15) / 16, nk), dim3(NT), 0, st, e->labels.as<int32_t>(),
                          e->grp_begin.as<int>(), e->grp_list.as<int>(), n, dcounts);
     }
@@ -572,7 +682,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     if (out->counts && !out->counts_on_device)
       HCHECK(hipMemcpyAsync(out->counts, dcounts, sizeof(int32_t) * cnt_len, hipMemcpyDeviceToHost, st));
   }
-  std::vector<int> si(nj), sr(nj);
+  std::vector<int> sr(nj);
   HCHECK(hipMemcpyAsync(si.data(), e->stop_iter.p, sizeof(int) * nj, hipMemcpyDeviceToHost, st));
   HCHECK(hipMemcpyAsync(sr.data(), e->stop_reason.p, sizeof(int) * nj, hipMemcpyDeviceToHost, st));
   if (out && out->labels)
@@ -583,39 +693,39 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   long long tot_iters = 0;
   int max_it = 0;
   double fl_wta = 0, fl_ahtw = 0;
-  for (int qq = 0; qq < nj; ++qq) {
-    const int itr = si[qq] ? si[qq] : iters_done;
+  for (int rid = 0; rid < nj; ++rid) {
+    const int itr = si[rid] ? si[rid] : iters_enqueued;
     tot_iters += itr;
     max_it = std::max(max_it, itr);
-    const double k = ri[qq].k;
+    const double k = all[rid].k;
     // algorithmic flops (nmf_mu.c:174-202 at 2*M*N*K each): W^T A + W^T W  |  A h^T + W0 (h h^T)
     fl_wta += (double)itr * (2.0 * m * n * k + 2.0 * m * k * k);
     fl_ahtw += (double)itr * (2.0 * m * n * k + 2.0 * m * k * k);
-    if (out && out->iters) out->iters[rslot[qq]] = itr;
-    if (out && out->stopped_early) out->stopped_early[rslot[qq]] = (sr[qq] == 1);
+    if (out && out->iters) out->iters[rslot[rid]] = itr;
+    if (out && out->stopped_early) out->stopped_early[rslot[rid]] = (sr[rid] == 1);
   }
   if (e->kcount[KID_WTA]) e->kflops[KID_WTA] = fl_wta / e->kcount[KID_WTA];
   if (e->kcount[KID_AHTW]) e->kflops[KID_AHTW] = fl_ahtw / e->kcount[KID_AHTW];
 
   if (out && (out->W || out->H)) {
-    std::vector<long> woff(nj + 1, 0), hoff(nj + 1, 0);
+    std::vector<long> woff(nj + 1, 0), ho(nj + 1, 0);
     for (int s = 0; s < nj; ++s) {
       woff[s + 1] = woff[s] + (long)m * job_k(s);
-      hoff[s + 1] = hoff[s] + (long)job_k(s) * n;
+      ho[s + 1] = ho[s] + (long)job_k(s) * n;
     }
     std::vector<double> hrow;
-    for (int qq = 0; qq < nj; ++qq) {
-      const int s = rslot[qq], k = ri[qq].k;
+    for (int rid = 0; rid < nj; ++rid) {
+      const int s = rslot[rid], k = all[rid].k;
       if (out->W)
-        HCHECK(hipMemcpy2DAsync(out->W + woff[s], sizeof(double) * m, e->W.as<double>() + (long)ri[qq].col0 * e->m_pad,
+        HCHECK(hipMemcpy2DAsync(out->W + woff[s], sizeof(double) * m, e->Wfin.as<double>() + (long)hoff[rid] * e->m_pad,
                                 sizeof(double) * e->m_pad, sizeof(double) * m, k, hipMemcpyDeviceToHost, st));
       if (out->H) {
         hrow.assign((size_t)k * n, 0.0);
-        HCHECK(hipMemcpy2DAsync(hrow.data(), sizeof(double) * n, e->H.as<double>() + (long)ri[qq].col0 * e->n_pad,
+        HCHECK(hipMemcpy2DAsync(hrow.data(), sizeof(double) * n, e->Hfin.as<double>() + (long)hoff[rid] * e->n_pad,
                                 sizeof(double) * e->n_pad, sizeof(double) * n, k, hipMemcpyDeviceToHost, st));
         HCHECK(hipStreamSynchronize(st));
         for (int j = 0; j < n; ++j)
-          for (int a = 0; a < k; ++a) out->H[hoff[s] + (long)j * k + a] = hrow[(size_t)a * n + j];
+          for (int a = 0; a < k; ++a) out->H[ho[s] + (long)j * k + a] = hrow[(size_t)a * n + j];
       }
     }
     HCHECK(hipStreamSynchronize(st));
@@ -628,8 +738,9 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     out->max_iter_run = max_it;
   }
   if (opts.verbose) {
-    fprintf(stderr, "[nmfc] %d restarts in %d panels, %d iterations enqueued, max %d, mean %.1f, %.3f s\n", nj, npanels,
-            iters_done, max_it, (double)tot_iters / nj, std::chrono::duration<double>(t_end - t_start).count());
+    fprintf(stderr, "[nmfc] %d restarts, %d iterations enqueued, max %d, mean %.1f, %d repacks, %.3f s\n", nj,
+            iters_enqueued, max_it, (double)tot_iters / nj, e->repacks,
+            std::chrono::duration<double>(t_end - t_start).count());
   }
   return 0;
 }
@@ -647,8 +758,7 @@ int nmfc_consensus(const double* Hs, int k, int n, int R, int label_rule, int32_
   std::vector<RestartInfo> ri(R);
   std::vector<int> slot(R), gb = {0, R};
   for (int r = 0; r < R; ++r) {
-    ri[r].col0 = r * k;
-    ri[r].k = k;
+    ri[r] = {r * k, k, r, 0};
     slot[r] = r;
   }
   DevBuf dH, dri, dslot, dgb, dlab, dcnt, dcons;

@@ -1,13 +1,15 @@
 // nmfc_kernels.hpp -- HIP kernels of the batched MU restart engine (gfx950 / CDNA4).
 //
 // Device layouts (DESIGN.md "Data layout in HBM"):
-//   Acm [n_cols_pad][m_pad]  column j of A, K(=gene)-contiguous        (operand of W^T A)
-//   Arm [m_pad][n_pad]       row i of A, K(=sample)-contiguous          (operand of A H^T)
-//   W   [Kt_pad][m_pad]      column c of the stacked W_all (restart r owns columns col0..col0+k-1)
-//   H   [Kt_pad][n_pad]      row c of the stacked H_all (row-major, sample-contiguous)
-//   restarts are packed into panels of 64 columns; a restart never straddles a panel.
-// Both big contractions are "TN" tiles: C[r][c] = sum_k P[r][k] * Q[c][k] with K-contiguous rows,
-// computed with v_mfma_f64_16x16x4_f64 from LDS-staged 64x32 tiles.
+//   Acm [n_cols_pad][m_pad]  column j of A, gene-contiguous              (operand of W^T A)
+//   Arm [m_pad][n_pad]       row i of A, sample-contiguous              (operand of A h^T)
+//   W   [cols][m_pad]        column c of the stacked W_all (restart owns columns col0..col0+k-1)
+//   H   [cols][n_pad]        row c of the stacked H_all (sample-contiguous)
+//   Restarts are packed into panels of 64 columns; a restart never straddles a panel.
+// Both contractions are "TN" tiles C[r][c] = sum_k P[r][k] Q[c][k] over K-contiguous rows, computed
+// with v_mfma_f64_16x16x4_f64 from LDS stages of 32 doubles per row (256 B rows, no padding) with an
+// XOR swizzle of the 16-byte slots (slot ^ (row & 11)) that makes the ds_read_b128 fragment reads
+// bank-conflict free (DESIGN.md "LDS layout").
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,12 +19,12 @@ namespace nmfc {
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-constexpr int TILE = 64;           // output tile edge == panel width (restart columns)
-constexpr int BK = 32;             // K depth of one LDS stage
-constexpr int LDSS = BK + 2;       // LDS row stride (doubles): 272 B rows -> conflict-free b64 fragment reads
-constexpr int NT = 256;            // threads per workgroup (4 waves, 2x2 over the 64x64 tile)
+constexpr int PANEL = 64;          // restart columns per panel
+constexpr int BK = 32;             // K depth of one LDS stage (one 256 B row per tile row)
+constexpr int NT = 256;            // threads per workgroup
 constexpr int HCH = 256;           // sample chunk of the H-update kernel
-constexpr int KMAX = 16;           // largest rank k handled by the H-update LDS arrays
+constexpr int KMAX = 16;           // largest rank k
+constexpr int GT = 128;            // genes per A h^T tile (and per Gram partial)
 constexpr int STOP_FIXED = 0, STOP_REF_COMPAT = 1, STOP_ARGMAX_STABLE = 2;
 constexpr double DIV_BY_ZERO_AVOIDANCE = 1E-09;   // nmf_mu.c:56
 
@@ -35,182 +37,291 @@ __device__ __forceinline__ double mu_rule(double old, double num, double den) {
   return t < 0.0 ? 0.0 : t;
 }
 
-// One 64x64 fp64 output tile, K range [kbeg, kend) (multiple of BK), 256 threads.
-// acc[mb][nb] holds the 16x16 block (wr*32+mb*16, wc*32+nb*16) of the wave's 32x32 quadrant.
-// C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg.
-__device__ __forceinline__ void tile_tn_f64(const double* __restrict__ P, long ldp, const double* __restrict__ Q,
-                                            long ldq, int kbeg, int kend, double* __restrict__ smem,
-                                            d4 (&acc)[2][2]) {
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, l = tid & 63;
-  const int wr = w >> 1, wc = w & 1;
-  double* Ps = smem;
-  double* Qs = smem + 2 * TILE * LDSS;
-  const int lrow = w * 16 + (l >> 4);
-  const int lch = (l & 15) * 2;
-  d2 pr[4], qr[4];
-  const int nst = (kend - kbeg) / BK;
-
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = lrow + 4 * i;
-    pr[i] = *reinterpret_cast<const d2*>(P + (long)row * ldp + kbeg + lch);
-    qr[i] = *reinterpret_cast<const d2*>(Q + (long)row * ldq + kbeg + lch);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = lrow + 4 * i;
-    *reinterpret_cast<d2*>(Ps + row * LDSS + lch) = pr[i];
-    *reinterpret_cast<d2*>(Qs + row * LDSS + lch) = qr[i];
-  }
-  __syncthreads();
-
-  const int fr = l & 15, fk = l >> 4;
-  for (int s = 0; s < nst; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nst) {
-      const int k0 = kbeg + (s + 1) * BK;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = lrow + 4 * i;
-        pr[i] = *reinterpret_cast<const d2*>(P + (long)row * ldp + k0 + lch);
-        qr[i] = *reinterpret_cast<const d2*>(Q + (long)row * ldq + k0 + lch);
-      }
-    }
-    const double* Pb = Ps + buf * TILE * LDSS;
-    const double* Qb = Qs + buf * TILE * LDSS;
-#pragma unroll
-    for (int kk = 0; kk < BK / 4; ++kk) {
-      const int kc = kk * 4 + fk;
-      const double a0 = Pb[(wr * 32 + fr) * LDSS + kc];
-      const double a1 = Pb[(wr * 32 + 16 + fr) * LDSS + kc];
-      const double b0 = Qb[(wc * 32 + fr) * LDSS + kc];
-      const double b1 = Qb[(wc * 32 + 16 + fr) * LDSS + kc];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (s + 1 < nst) {
-      double* Pn = Ps + (buf ^ 1) * TILE * LDSS;
-      double* Qn = Qs + (buf ^ 1) * TILE * LDSS;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = lrow + 4 * i;
-        *reinterpret_cast<d2*>(Pn + row * LDSS + lch) = pr[i];
-        *reinterpret_cast<d2*>(Qn + row * LDSS + lch) = qr[i];
-      }
-    }
-    __syncthreads();
-  }
+// Workgroup id -> work item such that each XCD (blocks b, b+8, ... share one) receives a contiguous
+// range of items (bijective for any count; a speed choice only, never correctness).
+__device__ __forceinline__ int xcd_item(int b, int nblocks) {
+  const int xcd = b & 7, idx = b >> 3;
+  const int q = nblocks >> 3, r = nblocks & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-__device__ __forceinline__ int acc_row(int wr, int mb, int l, int reg) { return wr * 32 + mb * 16 + (l >> 4) + 4 * reg; }
-__device__ __forceinline__ int acc_col(int wc, int nb, int l) { return wc * 32 + nb * 16 + (l & 15); }
+// ---------------------------------------------------------------------------------------------
+// The MFMA tile: RP x RQ outputs, 4 waves arranged WR x WC, K range [kbeg, kend) in stages of BK.
+// DB: double-buffered LDS stages; otherwise one stage buffer + register prefetch (less LDS, so two
+// workgroups share a CU and one's epilogue overlaps the other's MFMA loop).
+// ---------------------------------------------------------------------------------------------
+template <int RP, int RQ, int WR, int WC, bool DB>
+struct Tile {
+  static_assert(WR * WC == 4, "4 waves");
+  static constexpr int MB = RP / WR / 16;            // 16x16 blocks per wave, rows
+  static constexpr int NB = RQ / WC / 16;            // 16x16 blocks per wave, cols
+  static constexpr int PL = RP / 16;                 // 16-byte loads per lane per stage for P
+  static constexpr int QL = RQ / 16;
+  static constexpr int STAGE = (RP + RQ) * BK;       // doubles per LDS stage
+  static constexpr int LDS_DOUBLES = DB ? 2 * STAGE : STAGE;
 
-// A panel takes part in an iteration when one of its restarts is still running, or (for the
-// W update) stopped at exactly this iteration.
+  d4 acc[MB][NB];
+  d2 pr[PL], qr[QL];
+
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+  }
+
+  // one wave-instruction moves 4 rows x 256 B; lane l -> row (l >> 4), 16-byte slot (l & 15)
+  __device__ __forceinline__ void gload(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
+                                        int k0) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int slot2 = (l & 15) * 2;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const int row = i * 16 + w * 4 + (l >> 4);
+      pr[i] = *reinterpret_cast<const d2*>(P + (long)row * ldp + k0 + slot2);
+    }
+#pragma unroll
+    for (int i = 0; i < QL; ++i) {
+      const int row = i * 16 + w * 4 + (l >> 4);
+      qr[i] = *reinterpret_cast<const d2*>(Q + (long)row * ldq + k0 + slot2);
+    }
+  }
+
+  __device__ __forceinline__ void swrite(double* __restrict__ st) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int slot = l & 15;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const int row = i * 16 + w * 4 + (l >> 4);
+      *reinterpret_cast<d2*>(st + row * BK + ((slot ^ (row & 11)) << 1)) = pr[i];
+    }
+    double* sq = st + RP * BK;
+#pragma unroll
+    for (int i = 0; i < QL; ++i) {
+      const int row = i * 16 + w * 4 + (l >> 4);
+      *reinterpret_cast<d2*>(sq + row * BK + ((slot ^ (row & 11)) << 1)) = qr[i];
+    }
+  }
+
+  // lane group g = l >> 4 covers k = 8g + 2*kk2 + {0,1}: one ds_read_b128 per fragment and k pair
+  __device__ __forceinline__ void compute(const double* __restrict__ st) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int wr = w / WC, wc = w % WC;
+    const int fr = l & 15, g = l >> 4;
+    const int sw = fr & 11;
+    const double* sp = st + (wr * (RP / WR) + fr) * BK;
+    const double* sq = st + RP * BK + (wc * (RQ / WC) + fr) * BK;
+#pragma unroll
+    for (int kk2 = 0; kk2 < 4; ++kk2) {
+      const int off = (((4 * g + kk2) ^ sw) << 1);
+      d2 a[MB], b[NB];
+#pragma unroll
+      for (int i = 0; i < MB; ++i) a[i] = *reinterpret_cast<const d2*>(sp + i * 16 * BK + off);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) b[j] = *reinterpret_cast<const d2*>(sq + j * 16 * BK + off);
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+    }
+  }
+
+  __device__ __forceinline__ void run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
+                                      int kbeg, int kend, double* __restrict__ smem) {
+    const int nst = (kend - kbeg) / BK;
+    gload(P, ldp, Q, ldq, kbeg);
+    swrite(smem);
+    __syncthreads();
+    for (int s = 0; s < nst; ++s) {
+      const bool more = s + 1 < nst;
+      if (more) gload(P, ldp, Q, ldq, kbeg + (s + 1) * BK);
+      if (DB) {
+        compute(smem + (s & 1) * STAGE);
+        if (more) swrite(smem + ((s + 1) & 1) * STAGE);
+        __syncthreads();
+      } else {
+        compute(smem);
+        __syncthreads();
+        if (more) {
+          swrite(smem);
+          __syncthreads();
+        }
+      }
+    }
+  }
+
+  // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+  __device__ __forceinline__ static int row_of(int mb, int reg) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    return (w / WC) * (RP / WR) + mb * 16 + (l >> 4) + 4 * reg;
+  }
+  __device__ __forceinline__ static int col_of(int nb) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    return (w % WC) * (RQ / WC) + nb * 16 + (l & 15);
+  }
+};
+
+// Per-restart metadata.  rid is the persistent restart index (stop state, Gram/SH offsets, output
+// slot); col0 is its current first column in W/H (changes when the engine repacks live restarts).
+struct RestartInfo {
+  int col0;
+  int k;
+  int rid;
+  int sq_off;   // offset of its k x k blocks in the compact Gram / SH arrays
+};
+
+// A panel takes part when one of its restarts is still running, or (for the W update) stopped at
+// exactly this iteration.  [prb[p], pre[p]) is the panel's range in the active restart list.
 __device__ __forceinline__ bool panel_live(const int* __restrict__ prb, const int* __restrict__ pre, int p,
-                                           const int* __restrict__ stop_iter, int iter) {
+                                           const RestartInfo* __restrict__ ri, const int* __restrict__ stop_iter,
+                                           int iter) {
   const int b = prb[p], e = pre[p];
-  for (int r = b; r < e; ++r) {
-    const int s = stop_iter[r];
+  for (int q = b; q < e; ++q) {
+    const int s = stop_iter[ri[q].rid];
     if (s == 0 || s == iter) return true;
   }
   return false;
 }
 
 // ---------------------------------------------------------------------------------------------
-// K1 "wta":  G = W^T A  (nmf_mu.c:174) and SW = W_p^T W_p (nmf_mu.c:176) for every live panel.
-// grid = nsplit x npanels x (ntj + 1); column tile t == ntj is the panel Gram tile.  The gene
-// range is cut into fixed chunks (a function of m only), so the reduction order of every entry is
-// independent of batch composition; partials are summed in chunk order by K2.
+// K1 "wta":  G = W^T A  (nmf_mu.c:174), 128 x 128 tiles over (panel pair, sample tile); the gene
+// range is cut into fixed chunks (a function of m only, so each entry's summation order is
+// independent of batch composition); partials are summed in chunk order by k_hupdate.
 // ---------------------------------------------------------------------------------------------
-static __global__ __launch_bounds__(NT) void k_wta(const double* __restrict__ W, const double* __restrict__ Acm, long m_pad,
-                                            int npanels, int ntj, int kchunk, const int* __restrict__ prb,
-                                            const int* __restrict__ pre, const int* __restrict__ stop_iter, int iter,
-                                            double* __restrict__ Gpart, long g_ld, long g_split,
-                                            double* __restrict__ SWpart, long sw_split) {
-  __shared__ __attribute__((aligned(16))) double smem[4 * TILE * LDSS];
-  const int ntiles = ntj + 1;
-  const int b = blockIdx.x;
-  const int t = b % ntiles;
-  const int rest = b / ntiles;
-  const int p = rest % npanels;
-  const int s = rest / npanels;
-  if (!panel_live(prb, pre, p, stop_iter, 0x7fffffff) ) return;   // only still-running restarts
-  const double* P = W + (long)p * TILE * m_pad;
-  const bool gram = (t == ntj);
-  const double* Q = gram ? P : Acm + (long)t * TILE * m_pad;
+using TileH = Tile<128, 128, 2, 2, true>;
+
+static __global__ __launch_bounds__(NT) void k_wta(const double* __restrict__ W, const double* __restrict__ Acm,
+                                                   long m_pad, int npairs, int ntj, int nsplit, int kchunk,
+                                                   const int* __restrict__ prb, const int* __restrict__ pre,
+                                                   const RestartInfo* __restrict__ ri, const int* __restrict__ stop_iter,
+                                                   double* __restrict__ Gpart, long g_ld, long g_split) {
+  __shared__ __attribute__((aligned(16))) double smem[TileH::LDS_DOUBLES];
+  const int nitems = nsplit * npairs * ntj;
+  const int item = xcd_item(blockIdx.x, nitems);
+  const int t = item % ntj;
+  const int pp = (item / ntj) % npairs;
+  const int s = item / (ntj * npairs);
+  if (!panel_live(prb, pre, 2 * pp, ri, stop_iter, 0) && !panel_live(prb, pre, 2 * pp + 1, ri, stop_iter, 0)) return;
+  const double* P = W + (long)pp * 128 * m_pad;
+  const double* Q = Acm + (long)t * 128 * m_pad;
   const int kbeg = s * kchunk;
-  const int kend = min((long)kbeg + kchunk, m_pad);
-  d4 acc[2][2];
+  const int kend = (int)min((long)kbeg + kchunk, m_pad);
+  TileH tl;
+  tl.zero();
+  tl.run(P, m_pad, Q, m_pad, kbeg, kend, smem);
+  double* out = Gpart + (long)s * g_split + (long)pp * 128 * g_ld + (long)t * 128;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int mb = 0; mb < TileH::MB; ++mb)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
-  tile_tn_f64(P, m_pad, Q, m_pad, kbeg, kend, smem, acc);
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
-  double* out;
-  long ld;
-  if (gram) {
-    out = SWpart + (long)s * sw_split + (long)p * TILE * TILE;
-    ld = TILE;
-  } else {
-    out = Gpart + (long)s * g_split + (long)p * TILE * g_ld + (long)t * TILE;
-    ld = g_ld;
-  }
+    for (int nb = 0; nb < TileH::NB; ++nb)
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) out[(long)acc_row(wr, mb, l, reg) * ld + acc_col(wc, nb, l)] = acc[mb][nb][reg];
-  (void)iter;
+      for (int reg = 0; reg < 4; ++reg)
+        out[(long)TileH::row_of(mb, reg) * g_ld + TileH::col_of(nb)] = tl.acc[mb][nb][reg];
 }
 
 // ---------------------------------------------------------------------------------------------
-// K2 "hupdate": one workgroup per running restart.
-//   work2 = SW * H (nmf_mu.c:178); H <- mu_rule(H, G, work2) (:184-191); SH = H H^T (:200);
-//   stability check on the new H at even iterations (:253-282).
+// Gram partials: for every running restart of panel p and the GT genes of tile gt,
+// SWpart[gt][sq_off + a*k + b] = sum_{i in tile} W[c0+a][i] W[c0+b][i]  (i ascending), read from an
+// LDS image Wl[64][WLS] of the panel's (new) W.  k_hupdate sums the tiles in order: that is
+// work1 = W0^T W0 of nmf_mu.c:176 for the next iteration.
 // ---------------------------------------------------------------------------------------------
-struct RestartInfo {
-  int col0;   // first global column of the restart in W / H
-  int k;
-};
+constexpr int WLS = GT + 1;   // LDS row stride of the W image
 
-static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, int stop_rule, const RestartInfo* __restrict__ ri,
-                                                int n, long n_pad, const double* __restrict__ Gpart, long g_ld,
-                                                long g_split, int nsplit, const double* __restrict__ SWpart,
-                                                long sw_split, double* __restrict__ H, double* __restrict__ SHp,
-                                                int* __restrict__ stop_iter, int* __restrict__ stop_reason,
-                                                int* __restrict__ unchanged, int* __restrict__ classes, long cls_ld,
-                                                int* __restrict__ n_stopped) {
+__device__ __forceinline__ void gram_partials(const double* __restrict__ Wl, int p, int gt, const int* __restrict__ prb,
+                                              const int* __restrict__ pre, const RestartInfo* __restrict__ ri,
+                                              const int* __restrict__ stop_iter, double* __restrict__ SWpart,
+                                              long sw_total) {
+  const int b0 = prb[p], e0 = pre[p];
+  const int tid = threadIdx.x;
+  int off = 0;   // global pair index of the current restart's first pair; thread tid takes tid, tid+NT, ...
+  for (int q = b0; q < e0; ++q) {
+    const RestartInfo r = ri[q];
+    const int np = r.k * (r.k + 1) / 2;
+    if (stop_iter[r.rid] == 0) {
+      const int first = off + (((tid - off) % NT) + NT) % NT;
+      for (int gi = first; gi < off + np; gi += NT) {
+        int a = 0, tt = gi - off;
+        while (tt >= r.k - a) {
+          tt -= r.k - a;
+          ++a;
+        }
+        const int b = a + tt;
+        const int lc = r.col0 - p * PANEL;
+        const double* wa = Wl + (lc + a) * WLS;
+        const double* wb = Wl + (lc + b) * WLS;
+        double s2 = 0.0;
+        for (int i = 0; i < GT; ++i) s2 = fma(wa[i], wb[i], s2);
+        double* o = SWpart + (long)gt * sw_total + r.sq_off;
+        o[a * r.k + b] = s2;
+        o[b * r.k + a] = s2;
+      }
+    }
+    off += np;
+  }
+}
+
+// initial Gram partials of the freshly initialised W (iteration 1 needs W0^T W0)
+static __global__ __launch_bounds__(NT) void k_gram(const double* __restrict__ W, long m_pad, int npanels, int ngt,
+                                                    const int* __restrict__ prb, const int* __restrict__ pre,
+                                                    const RestartInfo* __restrict__ ri,
+                                                    const int* __restrict__ stop_iter, double* __restrict__ SWpart,
+                                                    long sw_total) {
+  __shared__ double Wl[PANEL * WLS];
+  const int item = xcd_item(blockIdx.x, npanels * ngt);
+  const int gt = item % ngt, p = item / ngt;
+  if (!panel_live(prb, pre, p, ri, stop_iter, 0)) return;
+  for (int idx = threadIdx.x; idx < PANEL * GT; idx += NT) {
+    const int c = idx / GT, i = idx % GT;
+    Wl[c * WLS + i] = W[((long)p * PANEL + c) * m_pad + (long)gt * GT + i];
+  }
+  __syncthreads();
+  gram_partials(Wl, p, gt, prb, pre, ri, stop_iter, SWpart, sw_total);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2 "hupdate": one workgroup per active restart.
+//   work1 = W0^T W0 = sum of Gram partials (nmf_mu.c:176); work2 = work1 H0 (:178);
+//   H <- mu_rule(H, G, work2) (:184-191); SH = H H^T (:200); stability check (:253-282).
+// ---------------------------------------------------------------------------------------------
+static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, int stop_rule,
+                                                       const RestartInfo* __restrict__ ri, int n, long n_pad,
+                                                       const double* __restrict__ Gpart, long g_ld, long g_split,
+                                                       int nsplit, const double* __restrict__ SWpart, long sw_total,
+                                                       int ngt, double* __restrict__ H, double* __restrict__ SH,
+                                                       int* __restrict__ stop_iter, int* __restrict__ stop_reason,
+                                                       int* __restrict__ unchanged, int* __restrict__ classes,
+                                                       long cls_ld, int* __restrict__ n_stopped) {
   __shared__ double sw[KMAX * KMAX];
   __shared__ double Hc[KMAX * HCH];
   __shared__ double Hn[KMAX * HCH];
   __shared__ double win[KMAX * KMAX];
   __shared__ int changed;
-  const int r = blockIdx.x;
-  if (stop_iter[r] != 0) return;
+  const RestartInfo me = ri[blockIdx.x];
+  const int rid = me.rid;
+  if (stop_iter[rid] != 0) return;
   const int tid = threadIdx.x;
-  const int c0 = ri[r].col0, k = ri[r].k;
-  const int p = c0 / TILE, lc0 = c0 % TILE;
+  const int c0 = me.col0, k = me.k;
   const bool check = (stop_rule != STOP_FIXED) && iter > 1 && (iter % 2 == 0);
   if (tid == 0) changed = 0;
   for (int idx = tid; idx < k * k; idx += NT) {
-    const int a = idx / k, bb = idx % k;
-    const long off = (long)p * TILE * TILE + (long)(lc0 + a) * TILE + (lc0 + bb);
-    double sacc = SWpart[off];
-    for (int sp = 1; sp < nsplit; ++sp) sacc += SWpart[(long)sp * sw_split + off];
-    sw[a * KMAX + bb] = sacc;
+    const double* src = SWpart + me.sq_off + idx;
+    double sacc = src[0];
+    for (int g = 1; g < ngt; ++g) sacc += src[(long)g * sw_total];
+    sw[(idx / k) * KMAX + (idx % k)] = sacc;
   }
   for (int idx = tid; idx < KMAX * KMAX; idx += NT) win[idx] = 0.0;
   const int npairs = k * (k + 1) / 2;
   int pa = 0, pb = 0;
-  if (tid < npairs) {  // (pa, pb) = tid-th pair of the upper triangle, row-major
+  if (tid < npairs) {
     int t = tid;
-    while (t >= k - pa) { t -= k - pa; ++pa; }
+    while (t >= k - pa) {
+      t -= k - pa;
+      ++pa;
+    }
     pb = pa + t;
   }
   double shacc = 0.0;
@@ -225,14 +336,14 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
       double hn = 0.0;
       if (valid) {
         const long goff = (long)(c0 + a) * g_ld + j;
-        double g = Gpart[goff];
-        for (int sp = 1; sp < nsplit; ++sp) g += Gpart[(long)sp * g_split + goff];
+        double gsum = Gpart[goff];
+        for (int sp = 1; sp < nsplit; ++sp) gsum += Gpart[(long)sp * g_split + goff];
         double d = 0.0;
         for (int bb = 0; bb < k; ++bb) d = fma(sw[a * KMAX + bb], Hc[bb * HCH + tid], d);
-        hn = mu_rule(Hc[a * HCH + tid], g, d);
+        hn = mu_rule(Hc[a * HCH + tid], gsum, d);
         H[(long)(c0 + a) * n_pad + j] = hn;
         if (stop_rule == STOP_REF_COMPAT) {
-          // flat column-major index of (a, j) in the k x n buffer; window i reads [i*n, i*n+k)
+          // flat column-major index of (a, j) in the k x n buffer; window i reads [i*n, i*n + k)
           const long tf = (long)j * k + a;
           const long wi = tf / n;
           if (wi < k) {
@@ -245,7 +356,7 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
       if (a > 0 && hn > Hn[best * HCH + tid]) best = a;
     }
     if (check && stop_rule == STOP_ARGMAX_STABLE && valid) {
-      int* cl = classes + (long)r * cls_ld + j;
+      int* cl = classes + (long)rid * cls_ld + j;
       if (*cl != best) {
         *cl = best;
         changed = 1;
@@ -261,9 +372,8 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
     __syncthreads();
   }
   if (tid < npairs) {
-    double* sh = SHp + (long)p * TILE * TILE;
-    sh[(lc0 + pa) * TILE + (lc0 + pb)] = shacc;
-    sh[(lc0 + pb) * TILE + (lc0 + pa)] = shacc;
+    SH[me.sq_off + pa * k + pb] = shacc;
+    SH[me.sq_off + pb * k + pa] = shacc;
   }
   if (check && stop_rule == STOP_REF_COMPAT) {
     const int nwin = k < n ? k : n;
@@ -271,7 +381,7 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
       int c = 0;
       for (int jj = 1; jj < k; ++jj)
         if (win[tid * KMAX + jj] > win[tid * KMAX + jj - 1]) c = jj;
-      int* cl = classes + (long)r * cls_ld + tid;
+      int* cl = classes + (long)rid * cls_ld + tid;
       if (*cl != c) {
         *cl = c;
         changed = 1;
@@ -283,93 +393,148 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
     int reason = 0;
     if (check) {
       if (!changed) {
-        const int u = unchanged[r] + 1;
-        unchanged[r] = u;
+        const int u = unchanged[rid] + 1;
+        unchanged[rid] = u;
         if (u >= 200) reason = 1;   // nmf_mu.c:269-271
       } else {
-        unchanged[r] = 0;
+        unchanged[rid] = 0;
       }
     }
     if (!reason && iter >= maxiter) reason = 2;
     if (reason) {
-      stop_iter[r] = iter;
-      stop_reason[r] = reason;
+      stop_iter[rid] = iter;
+      stop_reason[rid] = reason;
       atomicAdd(n_stopped, 1);
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// K3 "ahtw": F = A h^T (nmf_mu.c:198) computed transposed per tile (rows = panel columns c, cols =
-// genes i), fused with work2w = W0 * (h h^T) (:202) and the W rule (:209-216), written in place.
-// grid = npanels x ngt (gene tiles fastest).
+// K3 "ahtw": F = A h^T (nmf_mu.c:198) computed transposed per tile (rows = the 64 columns of panel
+// p, cols = GT genes), fused with work2w = W0 (h h^T) (:202), the W rule (:209-216) written in
+// place, and the Gram partials of the new W for the next iteration.
 // ---------------------------------------------------------------------------------------------
-static __global__ __launch_bounds__(NT) void k_ahtw(int iter, const double* __restrict__ H, long n_pad,
-                                             const double* __restrict__ Arm, long m_pad, double* __restrict__ W,
-                                             const double* __restrict__ SHp, const int* __restrict__ pcol_start,
-                                             const int* __restrict__ pcol_k, const int* __restrict__ pcol_rest,
-                                             const int* __restrict__ prb, const int* __restrict__ pre,
-                                             const int* __restrict__ stop_iter, int ngt) {
-  __shared__ __attribute__((aligned(16))) double smem[4 * TILE * LDSS];
-  __shared__ int cs[TILE], ck[TILE], cact[TILE];
-  const int b = blockIdx.x;
-  const int g = b % ngt;
-  const int p = b / ngt;
-  if (!panel_live(prb, pre, p, stop_iter, iter)) return;
-  const double* P = H + (long)p * TILE * n_pad;
-  const double* Q = Arm + (long)g * TILE * n_pad;
-  d4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
-  tile_tn_f64(P, n_pad, Q, n_pad, 0, (int)n_pad, smem, acc);
+using TileW = Tile<64, 128, 1, 4, false>;
+constexpr int FLS = GT + 1;   // LDS row stride of the F / new-W image (== WLS)
+constexpr int AHTW_EPI = PANEL * FLS + PANEL * KMAX;
+constexpr int AHTW_LDS = (TileW::LDS_DOUBLES > AHTW_EPI) ? TileW::LDS_DOUBLES : AHTW_EPI;
 
-  // epilogue: W tile (64 panel columns x 64 genes) and the panel's h h^T blocks into LDS
-  constexpr int ES = TILE + 1;
-  double* Wl = smem;
-  double* Sl = smem + TILE * ES;
-  const int tid = threadIdx.x;
-  for (int idx = tid; idx < TILE * TILE; idx += NT) {
-    const int c = idx / TILE, i = idx % TILE;
-    Wl[c * ES + i] = W[((long)p * TILE + c) * m_pad + (long)g * TILE + i];
-    Sl[c * ES + i] = SHp[(long)p * TILE * TILE + idx];
+template <int K>
+__device__ __forceinline__ void w_update_restart(const RestartInfo& r, int p, int gt, int i, long m_pad,
+                                                 double* __restrict__ W, double* __restrict__ Fl,
+                                                 const double* __restrict__ SHl) {
+  const int lc = r.col0 - p * PANEL;
+  const long gcol = (long)gt * GT + i;
+  double w[K];
+#pragma unroll
+  for (int b = 0; b < K; ++b) w[b] = W[(long)(r.col0 + b) * m_pad + gcol];
+  const double* sh = SHl + lc * KMAX;   // this restart's k x k block, row stride KMAX
+  double wn[K];
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    double e = 0.0;
+#pragma unroll
+    for (int b = 0; b < K; ++b) e = fma(w[b], sh[a * KMAX + b], e);
+    wn[a] = mu_rule(w[a], Fl[(lc + a) * FLS + i], e);
   }
-  if (tid < TILE) {
-    const int pc = p * TILE + tid;
-    cs[tid] = pcol_start[pc];
-    ck[tid] = pcol_k[pc];
-    const int rr = pcol_rest[pc];
-    int act = 0;
-    if (rr >= 0) {
-      const int s = stop_iter[rr];
-      act = (s == 0 || s == iter);
-    }
-    cact[tid] = act;
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    W[(long)(r.col0 + a) * m_pad + gcol] = wn[a];
+    Fl[(lc + a) * FLS + i] = wn[a];
+  }
+}
+
+static __global__ __launch_bounds__(NT, 2) void k_ahtw(int iter, const double* __restrict__ H, long n_pad,
+                                                       const double* __restrict__ Arm, long m_pad,
+                                                       double* __restrict__ W, const double* __restrict__ SH,
+                                                       const int* __restrict__ prb, const int* __restrict__ pre,
+                                                       const RestartInfo* __restrict__ ri,
+                                                       const int* __restrict__ stop_iter, int npanels, int ngt,
+                                                       double* __restrict__ SWpart, long sw_total) {
+  __shared__ __attribute__((aligned(16))) double smem[AHTW_LDS];
+  const int item = xcd_item(blockIdx.x, npanels * ngt);
+  // bands of 8 panels, gene super-tiles of 8: neighbouring items share operands in L2
+  int p, gt;
+  {
+    const int SP = 8, SG = 8;
+    const int band = item / (SP * ngt);
+    const int rem = item % (SP * ngt);
+    const int bp = min(SP, npanels - band * SP);
+    const int sg = rem / (bp * SG);
+    const int gsz = min(SG, ngt - sg * SG);
+    const int w2 = rem - sg * bp * SG;
+    p = band * SP + w2 / gsz;
+    gt = sg * SG + w2 % gsz;
+  }
+  if (!panel_live(prb, pre, p, ri, stop_iter, iter)) return;
+  TileW tl;
+  tl.zero();
+  tl.run(H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GT * n_pad, n_pad, 0, (int)n_pad, smem);
+
+  // epilogue: F tile and the panel's compact h h^T blocks into LDS
+  double* Fl = smem;
+  double* SHl = smem + PANEL * FLS;
+#pragma unroll
+  for (int mb = 0; mb < TileW::MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < TileW::NB; ++nb)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) Fl[TileW::row_of(mb, reg) * FLS + TileW::col_of(nb)] = tl.acc[mb][nb][reg];
+  const int b0 = prb[p], e0 = pre[p];
+  for (int q = b0; q < e0; ++q) {
+    const RestartInfo r = ri[q];
+    const int lc = r.col0 - p * PANEL;
+    for (int idx = threadIdx.x; idx < r.k * r.k; idx += NT)
+      SHl[(lc + idx / r.k) * KMAX + (idx % r.k)] = SH[r.sq_off + idx];
   }
   __syncthreads();
-  const int l = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
-#pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int c = acc_row(wr, mb, l, reg);
-        const int i = acc_col(wc, nb, l);
-        if (!cact[c]) continue;
-        const int st = cs[c], kk = ck[c];
-        double e = 0.0;
-        for (int q = 0; q < kk; ++q) e = fma(Sl[c * ES + st + q], Wl[(st + q) * ES + i], e);
-        const double wn = mu_rule(Wl[c * ES + i], acc[mb][nb][reg], e);
-        W[((long)p * TILE + c) * m_pad + (long)g * TILE + i] = wn;
-      }
+  // update: thread = (gene i, half h); the panel's restarts alternate between the two halves
+  const int i = threadIdx.x & (GT - 1), h = threadIdx.x >> 7;
+  for (int q = b0 + h; q < e0; q += 2) {
+    const RestartInfo r = ri[q];
+    const int s = stop_iter[r.rid];
+    if (!(s == 0 || s == iter)) continue;
+    switch (r.k) {
+#define NMFC_WCASE(KV)                                     \
+  case KV:                                                 \
+    w_update_restart<KV>(r, p, gt, i, m_pad, W, Fl, SHl); \
+    break;
+      NMFC_WCASE(2) NMFC_WCASE(3) NMFC_WCASE(4) NMFC_WCASE(5) NMFC_WCASE(6) NMFC_WCASE(7) NMFC_WCASE(8)
+      NMFC_WCASE(9) NMFC_WCASE(10) NMFC_WCASE(11) NMFC_WCASE(12) NMFC_WCASE(13) NMFC_WCASE(14) NMFC_WCASE(15)
+      NMFC_WCASE(16)
+#undef NMFC_WCASE
+      default:
+        break;
+    }
+  }
+  __syncthreads();
+  // Gram partials of the new W for the still-running restarts
+  gram_partials(Fl, p, gt, prb, pre, ri, stop_iter, SWpart, sw_total);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Repacking (compaction of live restarts) and the final-factor archive: k rows per job.
+// ---------------------------------------------------------------------------------------------
+struct MoveJob {
+  int src_row;
+  int dst_row;
+  int k;
+};
+
+static __global__ __launch_bounds__(NT) void k_move_rows(const MoveJob* __restrict__ jobs, const double* __restrict__ src,
+                                                         long src_ld, double* __restrict__ dst, long dst_ld, long len) {
+  const MoveJob jb = jobs[blockIdx.x];
+  for (int a = 0; a < jb.k; ++a) {
+    const double* s = src + (long)(jb.src_row + a) * src_ld;
+    double* d = dst + (long)(jb.dst_row + a) * dst_ld;
+    for (long x = (long)blockIdx.y * NT + threadIdx.x; x < len; x += (long)gridDim.y * NT) d[x] = s[x];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
 // Init: generateMatrix(ran) (generatematrix.c:131-137) with randnumber (randnumber.c:34) over the
-// glibc TYPE_3 stream seeded per job.  Thread = (restart, chunk of CHUNK draws).  The chunk's start
-// state is J[c] * s_344 (mod 2^32), J[c] = M^(c*CHUNK) the 31x31 jump matrix of the lagged
+// glibc TYPE_3 stream seeded per job.  Thread = (restart, chunk of RCHUNK draws); the chunk's start
+// state is J[c] * s_344 (mod 2^32), J[c] = M^(c*RCHUNK) the 31x31 jump matrix of the lagged
 // recurrence r[i] = r[i-31] + r[i-3].
 // ---------------------------------------------------------------------------------------------
 constexpr int RCHUNK = 31 * 32;   // draws per thread (multiple of 31 for a statically indexed ring)
@@ -382,10 +547,10 @@ struct InitJob {
 };
 
 static __global__ __launch_bounds__(NT) void k_init(const InitJob* __restrict__ jobs, const int* __restrict__ chunk_job,
-                                             const int* __restrict__ chunk_idx, int total_chunks,
-                                             const uint32_t* __restrict__ jump, int m, int n, long m_pad, long n_pad,
-                                             int min_init, int max_init, double* __restrict__ W,
-                                             double* __restrict__ H) {
+                                                    const int* __restrict__ chunk_idx, int total_chunks,
+                                                    const uint32_t* __restrict__ jump, int m, int n, long m_pad,
+                                                    long n_pad, int min_init, int max_init, double* __restrict__ W,
+                                                    double* __restrict__ H) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= total_chunks) return;
   const InitJob jb = jobs[chunk_job[gid]];
@@ -461,8 +626,8 @@ static __global__ __launch_bounds__(NT) void k_init(const InitJob* __restrict__ 
 // Labels (nmf.r:128 / documented intent) and connectivity counts (nmf.r:140-141).
 // ---------------------------------------------------------------------------------------------
 static __global__ __launch_bounds__(NT) void k_labels(const RestartInfo* __restrict__ ri, const int* __restrict__ slot,
-                                               const double* __restrict__ H, long n_pad, int n, int rule,
-                                               int32_t* __restrict__ labels) {
+                                                      const double* __restrict__ H, long n_pad, int n, int rule,
+                                                      int32_t* __restrict__ labels) {
   const int r = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
@@ -480,8 +645,10 @@ static __global__ __launch_bounds__(NT) void k_labels(const RestartInfo* __restr
 }
 
 // counts[g][i + j*n] = sum over the group's restarts of [L[i] == L[j]]
-static __global__ __launch_bounds__(NT) void k_counts(const int32_t* __restrict__ labels, const int* __restrict__ grp_begin,
-                                               const int* __restrict__ grp_list, int n, int32_t* __restrict__ counts) {
+static __global__ __launch_bounds__(NT) void k_counts(const int32_t* __restrict__ labels,
+                                                      const int* __restrict__ grp_begin,
+                                                      const int* __restrict__ grp_list, int n,
+                                                      int32_t* __restrict__ counts) {
   const int gidx = blockIdx.z;
   const int i = blockIdx.x * 16 + (threadIdx.x & 15);
   const int j = blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -502,7 +669,7 @@ static __global__ void k_divide(const int32_t* __restrict__ counts, double denom
 
 // A (m x n, ld lda) -> Acm (column j at j*m_pad, zero padded) and Arm (row i at i*n_pad)
 static __global__ void k_layout_a(const double* __restrict__ A, long lda, int m, int n, long m_pad, long n_pad,
-                           double* __restrict__ Acm, double* __restrict__ Arm) {
+                                  double* __restrict__ Acm, double* __restrict__ Arm) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int j = blockIdx.y;
   if (i >= m) return;
@@ -515,8 +682,8 @@ static __global__ void k_layout_a(const double* __restrict__ A, long lda, int m,
 // calculateNorm (calculatenorm.c:44-78) and calculateMaxchange (calculatemaxchange.c:42-71)
 // ---------------------------------------------------------------------------------------------
 static __global__ __launch_bounds__(NT) void k_norm_partial(const double* __restrict__ a, const double* __restrict__ w,
-                                                     const double* __restrict__ h, double* __restrict__ d, int m,
-                                                     int n, int k, double* __restrict__ partial) {
+                                                            const double* __restrict__ h, double* __restrict__ d, int m,
+                                                            int n, int k, double* __restrict__ partial) {
   __shared__ double red[NT];
   const long len = (long)m * n;
   double ss = 0.0;
@@ -537,8 +704,9 @@ static __global__ __launch_bounds__(NT) void k_norm_partial(const double* __rest
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
-static __global__ __launch_bounds__(NT) void k_maxchange_partial(const double* __restrict__ mat, double* __restrict__ mat0,
-                                                          long len, double* __restrict__ partial) {
+static __global__ __launch_bounds__(NT) void k_maxchange_partial(const double* __restrict__ mat,
+                                                                 double* __restrict__ mat0, long len,
+                                                                 double* __restrict__ partial) {
   __shared__ double r0[NT], r1[NT];
   double mx0 = 0.0, mxd = 0.0;
   for (long idx = (long)blockIdx.x * NT + threadIdx.x; idx < len; idx += (long)gridDim.x * NT) {
