@@ -58,6 +58,13 @@ def lib() -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
+    # One HIP runtime per process: libnmf.so and torch both bind the SONAME libamdhip64.so.7.  If torch
+    # is importable, load it first so that a later torch.cuda call (bench.py, multi-GPU all-reduce) and
+    # the engine share torch's already-loaded runtime instead of torch failing to initialise a second one.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not found: the HIP engine is not built (python -m nmfconsensus_amd.build)")
     L = ctypes.CDLL(LIB_PATH)

@@ -5,8 +5,9 @@
 // one MI355X: all (k, restart) jobs of a shard are packed into 64-column panels of a stacked W/H,
 // and every MU iteration is three launches on one HIP stream:
 //   k_wta     G = W^T A                                          (fp64 MFMA, fixed gene chunks)
-//   k_hupdate W^T W from Gram partials, H update, H H^T, stability check (one workgroup per restart)
-//   k_ahtw    A h^T fused with W0 (h h^T), the W update and the next Gram partials (fp64 MFMA)
+//   k_wta     also the restart-diagonal blocks of W^T W (nmf_mu.c:176) from the same staged W
+//   k_hupdate W^T W from the chunk partials, H update, H H^T, stability check (one workgroup per restart)
+//   k_ahtw    A h^T fused with W0 (h h^T) and the W update (fp64 MFMA)
 // Restarts that stop are archived and the live ones repacked into fewer panels as the sweep goes.
 #include <hip/hip_runtime.h>
 
@@ -116,6 +117,7 @@ enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID
 struct Packing {
   std::vector<RestartInfo> ri;   // active list, panel-contiguous
   std::vector<int> prb, pre;     // per panel: [begin, end) in ri
+  std::vector<ColInfo> ci;       // per panel column
   int npanels = 0;
 };
 
@@ -146,6 +148,9 @@ Packing pack(const std::vector<RestartInfo>& in) {
     pk.prb = {0, 0};
     pk.pre = {0, 0};
   }
+  pk.ci.assign((size_t)pk.npanels * PANEL, ColInfo{0, 0, 0, 0});
+  for (const RestartInfo& r : pk.ri)
+    for (int a = 0; a < r.k; ++a) pk.ci[r.col0 + a] = ColInfo{r.sq_off, r.col0 % PANEL, r.k, r.rid};
   return pk;
 }
 
@@ -161,7 +166,7 @@ struct nmfc_engine {
   // per-run buffers (grow-only)
   DevBuf W[2], H[2], Gpart, SWpart, SH, Hfin, Wfin;
   DevBuf rinfo, stop_iter, stop_reason, unchanged, classes, n_stopped;
-  DevBuf prb, pre, moves, finfo;
+  DevBuf prb, pre, colinfo, moves, finfo;
   DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp;
   int jump_chunks = 0;
   int* h_stopped = nullptr;   // pinned, 2 slots
@@ -311,7 +316,7 @@ void nmfc_engine_destroy(nmfc_engine* e) {
   DevBuf* bufs[] = {&e->Acm,       &e->Arm,       &e->W[0],      &e->W[1],     &e->H[0],       &e->H[1],
                     &e->Gpart,     &e->SWpart,    &e->SH,        &e->Hfin,     &e->Wfin,       &e->rinfo,
                     &e->stop_iter, &e->stop_reason, &e->unchanged, &e->classes, &e->n_stopped, &e->prb,
-                    &e->pre,       &e->moves,     &e->finfo,     &e->initjobs, &e->chunk_job,  &e->chunk_idx,
+                    &e->pre,       &e->colinfo,   &e->moves,     &e->finfo,     &e->initjobs, &e->chunk_job,  &e->chunk_idx,
                     &e->jump,      &e->labels,    &e->slot,      &e->grp_begin, &e->grp_list,  &e->counts_tmp,
                     &e->cons_tmp};
   for (DevBuf* b : bufs) b->release();
@@ -411,13 +416,14 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   // ---- device buffers ----
   if (e->W[0].ensure(sizeof(double) * cap_cols * e->m_pad) || e->H[0].ensure(sizeof(double) * cap_cols * e->n_pad) ||
       e->W[1].ensure(sizeof(double) * cap_cols * e->m_pad) || e->H[1].ensure(sizeof(double) * cap_cols * e->n_pad) ||
-      e->Gpart.ensure(sizeof(double) * g_split * e->nsplit) || e->SWpart.ensure(sizeof(double) * sw_total * e->ngt) ||
+      e->Gpart.ensure(sizeof(double) * g_split * e->nsplit) || e->SWpart.ensure(sizeof(double) * sw_total * e->nsplit) ||
       e->SH.ensure(sizeof(double) * sw_total) || e->Hfin.ensure(sizeof(double) * fin_rows * e->n_pad) ||
       (want_w && e->Wfin.ensure(sizeof(double) * fin_rows * e->m_pad)) || e->rinfo.ensure(sizeof(RestartInfo) * nj) ||
       e->finfo.ensure(sizeof(RestartInfo) * nj) || e->stop_iter.ensure(sizeof(int) * nj) ||
       e->stop_reason.ensure(sizeof(int) * nj) || e->unchanged.ensure(sizeof(int) * nj) ||
       e->classes.ensure(sizeof(int) * nj * cls_ld) || e->n_stopped.ensure(sizeof(int)) ||
       e->prb.ensure(sizeof(int) * pk.npanels) || e->pre.ensure(sizeof(int) * pk.npanels) ||
+      e->colinfo.ensure(sizeof(ColInfo) * pk.npanels * PANEL) ||
       e->moves.ensure(sizeof(MoveJob) * nj) || e->labels.ensure(sizeof(int32_t) * (size_t)nj * n) ||
       e->slot.ensure(sizeof(int) * nj))
     return -1;
@@ -428,6 +434,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                           hipMemcpyHostToDevice, st));
     HCHECK(hipMemcpyAsync(e->prb.p, p.prb.data(), sizeof(int) * p.npanels, hipMemcpyHostToDevice, st));
     HCHECK(hipMemcpyAsync(e->pre.p, p.pre.data(), sizeof(int) * p.npanels, hipMemcpyHostToDevice, st));
+    HCHECK(hipMemcpyAsync(e->colinfo.p, p.ci.data(), sizeof(ColInfo) * p.ci.size(), hipMemcpyHostToDevice, st));
     return 0;
   };
   if (upload_packing(pk)) return -1;
@@ -503,15 +510,6 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     HCHECK(hipGetLastError());
     HCHECK(hipStreamSynchronize(st));   // host vectors cj/ci go out of scope
   }
-  // Gram partials of W0 for iteration 1
-  {
-    TimedLaunch tl(e, KID_INIT);
-    hipLaunchKernelGGL(k_gram, dim3(pk.npanels * e->ngt), dim3(NT), 0, st, e->W[0].as<double>(), e->m_pad, pk.npanels,
-                       e->ngt, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->stop_iter.as<int>(),
-                       e->SWpart.as<double>(), sw_total);
-  }
-  HCHECK(hipGetLastError());
-
   // archive rows of restarts (final H, and W when requested) from the current buffers
   std::vector<char> archived(nj, 0);
   auto archive = [&](const std::vector<RestartInfo>& list) -> int {
@@ -552,15 +550,17 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         const int iter = it + c;
         {
           TimedLaunch tl(e, KID_WTA);
-          hipLaunchKernelGGL(k_wta, dim3(grid_wta), dim3(NT), 0, st, e->W[cur].as<double>(), e->Acm.as<double>(),
+          auto kw = (ntj >= 4) ? k_wta<1, true> : (ntj >= 2) ? k_wta<2, false> : k_wta<4, false>;
+          hipLaunchKernelGGL(kw, dim3(grid_wta), dim3(NT), 0, st, e->W[cur].as<double>(), e->Acm.as<double>(),
                              e->m_pad, npairs, ntj, e->nsplit, e->kchunk, e->prb.as<int>(), e->pre.as<int>(),
-                             e->rinfo.as<RestartInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split);
+                             e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(),
+                             e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
         }
         {
           TimedLaunch tl(e, KID_HUPD);
           hipLaunchKernelGGL(k_hupdate, dim3(nact), dim3(NT), 0, st, iter, opts.maxiter, opts.stop_rule,
                              e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, e->nsplit,
-                             e->SWpart.as<double>(), sw_total, e->ngt, e->H[cur].as<double>(), e->SH.as<double>(),
+                             e->SWpart.as<double>(), sw_total, e->H[cur].as<double>(), e->SH.as<double>(),
                              e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->unchanged.as<int>(),
                              e->classes.as<int>(), cls_ld, e->n_stopped.as<int>());
         }
@@ -568,8 +568,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           TimedLaunch tl(e, KID_AHTW);
           hipLaunchKernelGGL(k_ahtw, dim3(grid_ahtw), dim3(NT), 0, st, iter, e->H[cur].as<double>(), e->n_pad,
                              e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(), e->SH.as<double>(),
-                             e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->stop_iter.as<int>(),
-                             pk.npanels, e->ngt, e->SWpart.as<double>(), sw_total);
+                             e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
+                             e->stop_iter.as<int>(), pk.npanels, e->ngt);
         }
       }
       HCHECK(hipGetLastError());

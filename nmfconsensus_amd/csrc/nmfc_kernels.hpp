@@ -61,7 +61,20 @@ struct Tile {
   static constexpr int LDS_DOUBLES = DB ? 2 * STAGE : STAGE;
 
   d4 acc[MB][NB];
-  d2 pr[PL], qr[QL];
+  d2 pr[DB ? 2 : 1][PL], qr[DB ? 2 : 1][QL];   // register prefetch sets (two: loads run 2 stages ahead)
+  // operand blocks as buffer resources: one 32-bit row offset per load, the K position in soffset
+  __amdgpu_buffer_rsrc_t rp, rq;
+  int vop[PL], voq[QL];
+
+  __device__ __forceinline__ void bind(const double* P, long ldp, const double* Q, long ldq) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(P), 0, (int)(RP * ldp * 8), 0x00020000);
+    rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Q), 0, (int)(RQ * ldq * 8), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < PL; ++i) vop[i] = (int)(((long)(i * 16 + w * 4 + (l >> 4)) * ldp + (l & 15) * 2) * 8);
+#pragma unroll
+    for (int i = 0; i < QL; ++i) voq[i] = (int)(((long)(i * 16 + w * 4 + (l >> 4)) * ldq + (l & 15) * 2) * 8);
+  }
 
   __device__ __forceinline__ void zero() {
 #pragma unroll
@@ -71,35 +84,31 @@ struct Tile {
   }
 
   // one wave-instruction moves 4 rows x 256 B; lane l -> row (l >> 4), 16-byte slot (l & 15)
-  __device__ __forceinline__ void gload(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
-                                        int k0) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int slot2 = (l & 15) * 2;
+  template <int SET = 0>
+  __device__ __forceinline__ void gload(int k0) {
+    const int so = k0 * 8;
 #pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      const int row = i * 16 + w * 4 + (l >> 4);
-      pr[i] = *reinterpret_cast<const d2*>(P + (long)row * ldp + k0 + slot2);
-    }
+    for (int i = 0; i < PL; ++i)
+      pr[SET][i] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rp, vop[i], so, 0));
 #pragma unroll
-    for (int i = 0; i < QL; ++i) {
-      const int row = i * 16 + w * 4 + (l >> 4);
-      qr[i] = *reinterpret_cast<const d2*>(Q + (long)row * ldq + k0 + slot2);
-    }
+    for (int i = 0; i < QL; ++i)
+      qr[SET][i] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rq, voq[i], so, 0));
   }
 
+  template <int SET = 0>
   __device__ __forceinline__ void swrite(double* __restrict__ st) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int slot = l & 15;
 #pragma unroll
     for (int i = 0; i < PL; ++i) {
       const int row = i * 16 + w * 4 + (l >> 4);
-      *reinterpret_cast<d2*>(st + row * BK + ((slot ^ (row & 11)) << 1)) = pr[i];
+      *reinterpret_cast<d2*>(st + row * BK + ((slot ^ (row & 11)) << 1)) = pr[SET][i];
     }
     double* sq = st + RP * BK;
 #pragma unroll
     for (int i = 0; i < QL; ++i) {
       const int row = i * 16 + w * 4 + (l >> 4);
-      *reinterpret_cast<d2*>(sq + row * BK + ((slot ^ (row & 11)) << 1)) = qr[i];
+      *reinterpret_cast<d2*>(sq + row * BK + ((slot ^ (row & 11)) << 1)) = qr[SET][i];
     }
   }
 
@@ -127,29 +136,72 @@ struct Tile {
       for (int i = 0; i < MB; ++i)
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+      if (DB) __builtin_amdgcn_sched_barrier(0);   // keep fragment loads from hoisting across k pairs
+    }
+  }
+
+  // Double-buffered LDS with loads two stages ahead (register sets 0/1 alternate with the stage
+  // parity); `extra(stage)` lets a kernel add work on the staged tile (k_wta's Gram blocks).
+  template <bool DEEP = true, class Extra>
+  __device__ __forceinline__ void run_db(const double* __restrict__ P, long ldp, const double* __restrict__ Q,
+                                         long ldq, int kbeg, int kend, double* __restrict__ smem, Extra extra) {
+    const int nst = (kend - kbeg) / BK;
+    double* b0 = smem;
+    double* b1 = smem + STAGE;
+    bind(P, ldp, Q, ldq);
+    if (!DEEP) {   // loads one stage ahead, one register set (lower register pressure)
+      gload<0>(kbeg);
+      swrite<0>(b0);
+      __syncthreads();
+      for (int s = 0; s < nst; ++s) {
+        const bool more = s + 1 < nst;
+        if (more) gload<0>(kbeg + (s + 1) * BK);
+        double* cur = (s & 1) ? b1 : b0;
+        compute(cur);
+        extra(cur);
+        if (more) swrite<0>((s & 1) ? b0 : b1);
+        __syncthreads();
+      }
+      return;
+    }
+    gload<0>(kbeg);
+    if (nst > 1) gload<1>(kbeg + BK);
+    swrite<0>(b0);
+    __syncthreads();
+    for (int s = 0; s < nst; s += 2) {
+      if (s + 2 < nst) gload<0>(kbeg + (s + 2) * BK);
+      compute(b0);
+      extra(b0);
+      if (s + 1 < nst) swrite<1>(b1);
+      __syncthreads();
+      if (s + 1 >= nst) break;
+      if (s + 3 < nst) gload<1>(kbeg + (s + 3) * BK);
+      compute(b1);
+      extra(b1);
+      if (s + 2 < nst) swrite<0>(b0);
+      __syncthreads();
     }
   }
 
   __device__ __forceinline__ void run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
                                       int kbeg, int kend, double* __restrict__ smem) {
+    if (DB) {
+      run_db(P, ldp, Q, ldq, kbeg, kend, smem, [](const double*) {});
+      return;
+    }
     const int nst = (kend - kbeg) / BK;
-    gload(P, ldp, Q, ldq, kbeg);
+    bind(P, ldp, Q, ldq);
+    gload(kbeg);
     swrite(smem);
     __syncthreads();
     for (int s = 0; s < nst; ++s) {
       const bool more = s + 1 < nst;
-      if (more) gload(P, ldp, Q, ldq, kbeg + (s + 1) * BK);
-      if (DB) {
-        compute(smem + (s & 1) * STAGE);
-        if (more) swrite(smem + ((s + 1) & 1) * STAGE);
+      if (more) gload(kbeg + (s + 1) * BK);
+      compute(smem);
+      __syncthreads();
+      if (more) {
+        swrite(smem);
         __syncthreads();
-      } else {
-        compute(smem);
-        __syncthreads();
-        if (more) {
-          swrite(smem);
-          __syncthreads();
-        }
       }
     }
   }
@@ -174,6 +226,15 @@ struct RestartInfo {
   int sq_off;   // offset of its k x k blocks in the compact Gram / SH arrays
 };
 
+// Per panel column: the owning restart's compact-block offset, its first panel-local column, k
+// (k = 0: padding column) and its restart id.
+struct ColInfo {
+  int sq_off;
+  int lc0;
+  int k;
+  int rid;
+};
+
 // A panel takes part when one of its restarts is still running, or (for the W update) stopped at
 // exactly this iteration.  [prb[p], pre[p]) is the panel's range in the active restart list.
 __device__ __forceinline__ bool panel_live(const int* __restrict__ prb, const int* __restrict__ pre, int p,
@@ -194,25 +255,106 @@ __device__ __forceinline__ bool panel_live(const int* __restrict__ prb, const in
 // ---------------------------------------------------------------------------------------------
 using TileH = Tile<128, 128, 2, 2, true>;
 
+// Gram blocks of a panel pair needed by restarts with k <= 16: per panel the diagonal 16x16 blocks
+// (b, b) and the straddling blocks (b, b+1); 14 candidates spread over the pair's ntj sample-tile
+// workgroups and their 4 waves: wave w of tile t takes candidates t + ntj * (w + 4x).
+constexpr int GRAM_CAND = 14;
+
+__device__ __forceinline__ void gram_block_of(int cand, int& q, int& br, int& bc) {
+  q = cand / 7;
+  const int x = cand % 7;
+  if (x < 4) {
+    br = x;
+    bc = x;
+  } else {
+    br = x - 4;
+    bc = x - 3;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1 "wta":  G = W^T A  (nmf_mu.c:174), 128 x 128 tiles over (panel pair, sample tile), and the
+// Gram W^T W (nmf_mu.c:176) restricted to the 16x16 blocks that carry restart-diagonal k x k blocks,
+// from the same LDS-staged W tile (a few extra MFMAs per wave, spread evenly).  The gene range is cut into fixed
+// chunks (a function of m only, so each entry's summation order is independent of batch
+// composition); per-chunk partials are summed in chunk order by k_hupdate.
+// ---------------------------------------------------------------------------------------------
+// GRAM_PER_WAVE = ceil(14 / (4 * ntj)) candidates per wave (1 for n > 384), chosen by the host.
+template <int GRAM_PER_WAVE, bool DEEP>
 static __global__ __launch_bounds__(NT) void k_wta(const double* __restrict__ W, const double* __restrict__ Acm,
                                                    long m_pad, int npairs, int ntj, int nsplit, int kchunk,
                                                    const int* __restrict__ prb, const int* __restrict__ pre,
-                                                   const RestartInfo* __restrict__ ri, const int* __restrict__ stop_iter,
-                                                   double* __restrict__ Gpart, long g_ld, long g_split) {
+                                                   const RestartInfo* __restrict__ ri, const ColInfo* __restrict__ ci,
+                                                   const int* __restrict__ stop_iter, double* __restrict__ Gpart,
+                                                   long g_ld, long g_split, double* __restrict__ SWpart,
+                                                   long sw_total) {
   __shared__ __attribute__((aligned(16))) double smem[TileH::LDS_DOUBLES];
+  __shared__ int need[GRAM_CAND];
   const int nitems = nsplit * npairs * ntj;
   const int item = xcd_item(blockIdx.x, nitems);
   const int t = item % ntj;
   const int pp = (item / ntj) % npairs;
   const int s = item / (ntj * npairs);
-  if (!panel_live(prb, pre, 2 * pp, ri, stop_iter, 0) && !panel_live(prb, pre, 2 * pp + 1, ri, stop_iter, 0)) return;
+  const bool live0 = panel_live(prb, pre, 2 * pp, ri, stop_iter, 0);
+  const bool live1 = panel_live(prb, pre, 2 * pp + 1, ri, stop_iter, 0);
+  if (!live0 && !live1) return;
+  if (threadIdx.x < GRAM_CAND) {
+    int q, br, bc;
+    gram_block_of(threadIdx.x, q, br, bc);
+    int nd = (q == 0) ? live0 : live1;
+    if (nd && br != bc) {   // straddling block: needed only if a restart spans columns 16*bc-1 and 16*bc
+      const ColInfo c = ci[(long)(2 * pp + q) * PANEL + 16 * bc];
+      nd = (c.k > 0 && c.lc0 < 16 * bc);
+    }
+    need[threadIdx.x] = nd;
+  }
   const double* P = W + (long)pp * 128 * m_pad;
   const double* Q = Acm + (long)t * 128 * m_pad;
   const int kbeg = s * kchunk;
   const int kend = (int)min((long)kbeg + kchunk, m_pad);
   TileH tl;
   tl.zero();
-  tl.run(P, m_pad, Q, m_pad, kbeg, kend, smem);
+  d4 gacc[GRAM_PER_WAVE];
+#pragma unroll
+  for (int x = 0; x < GRAM_PER_WAVE; ++x) gacc[x] = (d4){0.0, 0.0, 0.0, 0.0};
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int fr = l & 15, g = l >> 4, sw = fr & 11;
+  __syncthreads();   // need[] visible
+  int my_need[GRAM_PER_WAVE];
+  int my_ra[GRAM_PER_WAVE], my_rb[GRAM_PER_WAVE];
+  bool gram = false;
+#pragma unroll
+  for (int x = 0; x < GRAM_PER_WAVE; ++x) {
+    const int cand = t + ntj * (w + 4 * x);
+    my_need[x] = 0;
+    my_ra[x] = 0;
+    my_rb[x] = 0;
+    if (cand < GRAM_CAND) {
+      int q, br, bc;
+      gram_block_of(cand, q, br, bc);
+      my_need[x] = need[cand];
+      my_ra[x] = 64 * q + 16 * br;
+      my_rb[x] = 64 * q + 16 * bc;
+      gram = gram || my_need[x];
+    }
+  }
+  tl.template run_db<DEEP>(P, m_pad, Q, m_pad, kbeg, kend, smem, [&](const double* stg) {
+    if (!gram) return;
+#pragma unroll
+    for (int x = 0; x < GRAM_PER_WAVE; ++x) {
+      if (!my_need[x]) continue;
+      const double* pa = stg + (my_ra[x] + fr) * BK;
+      const double* pb = stg + (my_rb[x] + fr) * BK;
+#pragma unroll
+      for (int kk2 = 0; kk2 < 4; ++kk2) {
+        const int off = (((4 * g + kk2) ^ sw) << 1);
+        const d2 a = *reinterpret_cast<const d2*>(pa + off);
+        const d2 b = *reinterpret_cast<const d2*>(pb + off);
+        gacc[x] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b.x, gacc[x], 0, 0, 0);
+        gacc[x] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b.y, gacc[x], 0, 0, 0);
+      }
+    }
+  });
   double* out = Gpart + (long)s * g_split + (long)pp * 128 * g_ld + (long)t * 128;
 #pragma unroll
   for (int mb = 0; mb < TileH::MB; ++mb)
@@ -221,77 +363,37 @@ static __global__ __launch_bounds__(NT) void k_wta(const double* __restrict__ W,
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg)
         out[(long)TileH::row_of(mb, reg) * g_ld + TileH::col_of(nb)] = tl.acc[mb][nb][reg];
-}
-
-// ---------------------------------------------------------------------------------------------
-// Gram partials: for every running restart of panel p and the GT genes of tile gt,
-// SWpart[gt][sq_off + a*k + b] = sum_{i in tile} W[c0+a][i] W[c0+b][i]  (i ascending), read from an
-// LDS image Wl[64][WLS] of the panel's (new) W.  k_hupdate sums the tiles in order: that is
-// work1 = W0^T W0 of nmf_mu.c:176 for the next iteration.
-// ---------------------------------------------------------------------------------------------
-constexpr int WLS = GT + 1;   // LDS row stride of the W image
-
-__device__ __forceinline__ void gram_partials(const double* __restrict__ Wl, int p, int gt, const int* __restrict__ prb,
-                                              const int* __restrict__ pre, const RestartInfo* __restrict__ ri,
-                                              const int* __restrict__ stop_iter, double* __restrict__ SWpart,
-                                              long sw_total) {
-  const int b0 = prb[p], e0 = pre[p];
-  const int tid = threadIdx.x;
-  int off = 0;   // global pair index of the current restart's first pair; thread tid takes tid, tid+NT, ...
-  for (int q = b0; q < e0; ++q) {
-    const RestartInfo r = ri[q];
-    const int np = r.k * (r.k + 1) / 2;
-    if (stop_iter[r.rid] == 0) {
-      const int first = off + (((tid - off) % NT) + NT) % NT;
-      for (int gi = first; gi < off + np; gi += NT) {
-        int a = 0, tt = gi - off;
-        while (tt >= r.k - a) {
-          tt -= r.k - a;
-          ++a;
-        }
-        const int b = a + tt;
-        const int lc = r.col0 - p * PANEL;
-        const double* wa = Wl + (lc + a) * WLS;
-        const double* wb = Wl + (lc + b) * WLS;
-        double s2 = 0.0;
-        for (int i = 0; i < GT; ++i) s2 = fma(wa[i], wb[i], s2);
-        double* o = SWpart + (long)gt * sw_total + r.sq_off;
-        o[a * r.k + b] = s2;
-        o[b * r.k + a] = s2;
+  if (gram) {
+    double* so = SWpart + (long)s * sw_total;
+#pragma unroll
+    for (int x = 0; x < GRAM_PER_WAVE; ++x) {
+      if (!my_need[x]) continue;
+      const int pnl = my_ra[x] >> 6;   // panel within the pair
+      const ColInfo* cp = ci + (long)(2 * pp + pnl) * PANEL;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int lr = (my_ra[x] & 63) + g + 4 * reg;   // panel-local row column index
+        const int lcn = (my_rb[x] & 63) + fr;           // panel-local col column index
+        const ColInfo cr = cp[lr];
+        if (cr.k == 0 || cr.lc0 != cp[lcn].lc0 || cp[lcn].k == 0) continue;   // not the same restart
+        const int a = lr - cr.lc0, b = lcn - cr.lc0;
+        so[cr.sq_off + a * cr.k + b] = gacc[x][reg];
+        so[cr.sq_off + b * cr.k + a] = gacc[x][reg];
       }
     }
-    off += np;
   }
-}
-
-// initial Gram partials of the freshly initialised W (iteration 1 needs W0^T W0)
-static __global__ __launch_bounds__(NT) void k_gram(const double* __restrict__ W, long m_pad, int npanels, int ngt,
-                                                    const int* __restrict__ prb, const int* __restrict__ pre,
-                                                    const RestartInfo* __restrict__ ri,
-                                                    const int* __restrict__ stop_iter, double* __restrict__ SWpart,
-                                                    long sw_total) {
-  __shared__ double Wl[PANEL * WLS];
-  const int item = xcd_item(blockIdx.x, npanels * ngt);
-  const int gt = item % ngt, p = item / ngt;
-  if (!panel_live(prb, pre, p, ri, stop_iter, 0)) return;
-  for (int idx = threadIdx.x; idx < PANEL * GT; idx += NT) {
-    const int c = idx / GT, i = idx % GT;
-    Wl[c * WLS + i] = W[((long)p * PANEL + c) * m_pad + (long)gt * GT + i];
-  }
-  __syncthreads();
-  gram_partials(Wl, p, gt, prb, pre, ri, stop_iter, SWpart, sw_total);
 }
 
 // ---------------------------------------------------------------------------------------------
 // K2 "hupdate": one workgroup per active restart.
-//   work1 = W0^T W0 = sum of Gram partials (nmf_mu.c:176); work2 = work1 H0 (:178);
+//   work1 = W0^T W0 = sum of the per-chunk Gram partials (nmf_mu.c:176); work2 = work1 H0 (:178);
 //   H <- mu_rule(H, G, work2) (:184-191); SH = H H^T (:200); stability check (:253-282).
 // ---------------------------------------------------------------------------------------------
 static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, int stop_rule,
                                                        const RestartInfo* __restrict__ ri, int n, long n_pad,
                                                        const double* __restrict__ Gpart, long g_ld, long g_split,
                                                        int nsplit, const double* __restrict__ SWpart, long sw_total,
-                                                       int ngt, double* __restrict__ H, double* __restrict__ SH,
+                                                       double* __restrict__ H, double* __restrict__ SH,
                                                        int* __restrict__ stop_iter, int* __restrict__ stop_reason,
                                                        int* __restrict__ unchanged, int* __restrict__ classes,
                                                        long cls_ld, int* __restrict__ n_stopped) {
@@ -310,7 +412,7 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
   for (int idx = tid; idx < k * k; idx += NT) {
     const double* src = SWpart + me.sq_off + idx;
     double sacc = src[0];
-    for (int g = 1; g < ngt; ++g) sacc += src[(long)g * sw_total];
+    for (int g = 1; g < nsplit; ++g) sacc += src[(long)g * sw_total];
     sw[(idx / k) * KMAX + (idx % k)] = sacc;
   }
   for (int idx = tid; idx < KMAX * KMAX; idx += NT) win[idx] = 0.0;
@@ -411,47 +513,28 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
 
 // ---------------------------------------------------------------------------------------------
 // K3 "ahtw": F = A h^T (nmf_mu.c:198) computed transposed per tile (rows = the 64 columns of panel
-// p, cols = GT genes), fused with work2w = W0 (h h^T) (:202), the W rule (:209-216) written in
-// place, and the Gram partials of the new W for the next iteration.
+// p, cols = GT genes), fused with work2w = W0 (h h^T) (:202) and the W rule (:209-216), written in
+// place.  The epilogue runs in the MFMA accumulator layout (F never leaves registers); the W0 tile is
+// prefetched into registers during the last K stage and staged in LDS with the panel's h h^T blocks.
 // ---------------------------------------------------------------------------------------------
 using TileW = Tile<64, 128, 1, 4, false>;
-constexpr int FLS = GT + 1;   // LDS row stride of the F / new-W image (== WLS)
-constexpr int AHTW_EPI = PANEL * FLS + PANEL * KMAX;
+constexpr int WLS = GT + 2;        // LDS row stride of the W0 tile (16-byte aligned rows)
+constexpr int SHS = KMAX + 1;      // LDS row stride of the h h^T rows
+constexpr int AHTW_EPI = PANEL * WLS + PANEL * SHS;
 constexpr int AHTW_LDS = (TileW::LDS_DOUBLES > AHTW_EPI) ? TileW::LDS_DOUBLES : AHTW_EPI;
 
-template <int K>
-__device__ __forceinline__ void w_update_restart(const RestartInfo& r, int p, int gt, int i, long m_pad,
-                                                 double* __restrict__ W, double* __restrict__ Fl,
-                                                 const double* __restrict__ SHl) {
-  const int lc = r.col0 - p * PANEL;
-  const long gcol = (long)gt * GT + i;
-  double w[K];
-#pragma unroll
-  for (int b = 0; b < K; ++b) w[b] = W[(long)(r.col0 + b) * m_pad + gcol];
-  const double* sh = SHl + lc * KMAX;   // this restart's k x k block, row stride KMAX
-  double wn[K];
-#pragma unroll
-  for (int a = 0; a < K; ++a) {
-    double e = 0.0;
-#pragma unroll
-    for (int b = 0; b < K; ++b) e = fma(w[b], sh[a * KMAX + b], e);
-    wn[a] = mu_rule(w[a], Fl[(lc + a) * FLS + i], e);
-  }
-#pragma unroll
-  for (int a = 0; a < K; ++a) {
-    W[(long)(r.col0 + a) * m_pad + gcol] = wn[a];
-    Fl[(lc + a) * FLS + i] = wn[a];
-  }
-}
-
-static __global__ __launch_bounds__(NT, 2) void k_ahtw(int iter, const double* __restrict__ H, long n_pad,
+// PREF selects where the W0 prefetch is issued: 0 = during the last K stage, 1 = right after the
+// prologue (kept as a template switch for tools/kbench.hip).
+template <int PREF>
+static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double* __restrict__ H, long n_pad,
                                                        const double* __restrict__ Arm, long m_pad,
                                                        double* __restrict__ W, const double* __restrict__ SH,
                                                        const int* __restrict__ prb, const int* __restrict__ pre,
                                                        const RestartInfo* __restrict__ ri,
-                                                       const int* __restrict__ stop_iter, int npanels, int ngt,
-                                                       double* __restrict__ SWpart, long sw_total) {
+                                                       const ColInfo* __restrict__ ci,
+                                                       const int* __restrict__ stop_iter, int npanels, int ngt) {
   __shared__ __attribute__((aligned(16))) double smem[AHTW_LDS];
+  __shared__ int c_lc0[PANEL], c_k[PANEL], c_act[PANEL];
   const int item = xcd_item(blockIdx.x, npanels * ngt);
   // bands of 8 panels, gene super-tiles of 8: neighbouring items share operands in L2
   int p, gt;
@@ -467,50 +550,110 @@ static __global__ __launch_bounds__(NT, 2) void k_ahtw(int iter, const double* _
     gt = sg * SG + w2 % gsz;
   }
   if (!panel_live(prb, pre, p, ri, stop_iter, iter)) return;
+  const int tid = threadIdx.x;
+  const double* P = H + (long)p * PANEL * n_pad;
+  const double* Q = Arm + (long)gt * GT * n_pad;
+  const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GT;
   TileW tl;
   tl.zero();
-  tl.run(H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GT * n_pad, n_pad, 0, (int)n_pad, smem);
-
-  // epilogue: F tile and the panel's compact h h^T blocks into LDS
-  double* Fl = smem;
-  double* SHl = smem + PANEL * FLS;
+  d2 wpre[16];
+  const int nst = (int)(n_pad / BK);
+  tl.bind(P, n_pad, Q, n_pad);
+  tl.gload(0);
+  if (PREF == 1) {
 #pragma unroll
-  for (int mb = 0; mb < TileW::MB; ++mb)
+    for (int j = 0; j < 16; ++j)
+      wpre[j] = *reinterpret_cast<const d2*>(wsrc + (long)((tid >> 6) + 4 * j) * m_pad + (tid & 63) * 2);
+  }
+  tl.swrite(smem);
+  __syncthreads();
+  for (int st = 0; st + 1 < nst; ++st) {
+    tl.gload((st + 1) * BK);
+    tl.compute(smem);
+    __syncthreads();
+    tl.swrite(smem);
+    __syncthreads();
+  }
+  if (PREF == 0) {
+    // last stage: no staging load is in flight, so the W0 prefetch overlaps this stage's MFMAs
 #pragma unroll
-    for (int nb = 0; nb < TileW::NB; ++nb)
+    for (int j = 0; j < 16; ++j)
+      wpre[j] = *reinterpret_cast<const d2*>(wsrc + (long)((tid >> 6) + 4 * j) * m_pad + (tid & 63) * 2);
+  }
+  tl.compute(smem);
+  __syncthreads();
+  // epilogue staging: W0 tile, the panel's compact h h^T blocks, per-column restart info
+  double* Wl = smem;
+  double* SHl = smem + PANEL * WLS;
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) Fl[TileW::row_of(mb, reg) * FLS + TileW::col_of(nb)] = tl.acc[mb][nb][reg];
+  for (int j = 0; j < 16; ++j) *reinterpret_cast<d2*>(Wl + ((tid >> 6) + 4 * j) * WLS + (tid & 63) * 2) = wpre[j];
   const int b0 = prb[p], e0 = pre[p];
   for (int q = b0; q < e0; ++q) {
     const RestartInfo r = ri[q];
     const int lc = r.col0 - p * PANEL;
-    for (int idx = threadIdx.x; idx < r.k * r.k; idx += NT)
-      SHl[(lc + idx / r.k) * KMAX + (idx % r.k)] = SH[r.sq_off + idx];
+    for (int idx = tid; idx < r.k * r.k; idx += NT) SHl[(lc + idx / r.k) * SHS + (idx % r.k)] = SH[r.sq_off + idx];
   }
-  __syncthreads();
-  // update: thread = (gene i, half h); the panel's restarts alternate between the two halves
-  const int i = threadIdx.x & (GT - 1), h = threadIdx.x >> 7;
-  for (int q = b0 + h; q < e0; q += 2) {
-    const RestartInfo r = ri[q];
-    const int s = stop_iter[r.rid];
-    if (!(s == 0 || s == iter)) continue;
-    switch (r.k) {
-#define NMFC_WCASE(KV)                                     \
-  case KV:                                                 \
-    w_update_restart<KV>(r, p, gt, i, m_pad, W, Fl, SHl); \
-    break;
-      NMFC_WCASE(2) NMFC_WCASE(3) NMFC_WCASE(4) NMFC_WCASE(5) NMFC_WCASE(6) NMFC_WCASE(7) NMFC_WCASE(8)
-      NMFC_WCASE(9) NMFC_WCASE(10) NMFC_WCASE(11) NMFC_WCASE(12) NMFC_WCASE(13) NMFC_WCASE(14) NMFC_WCASE(15)
-      NMFC_WCASE(16)
-#undef NMFC_WCASE
-      default:
-        break;
+  if (tid < PANEL) {
+    const ColInfo c = ci[(long)p * PANEL + tid];
+    c_lc0[tid] = c.lc0;
+    c_k[tid] = c.k;
+    int act = 0;
+    if (c.k > 0) {
+      const int sv = stop_iter[c.rid];
+      act = (sv == 0 || sv == iter);
     }
+    c_act[tid] = act;
   }
   __syncthreads();
-  // Gram partials of the new W for the still-running restarts
-  gram_partials(Fl, p, gt, prb, pre, ri, stop_iter, SWpart, sw_total);
+  double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GT;
+  // E = W0 (h h^T) for the lane's 32 accumulator elements, b-outer so the 32 fma chains are
+  // independent (each chain still sums b = 0..k-1 in order, as the VALU reference does)
+  int lcs[TileW::MB][4], kss[TileW::MB][4];
+  int kmx = 0;
+#pragma unroll
+  for (int mb = 0; mb < TileW::MB; ++mb)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int c = TileW::row_of(mb, reg);
+      lcs[mb][reg] = c_lc0[c];
+      kss[mb][reg] = c_act[c] ? c_k[c] : 0;
+      kmx = max(kmx, kss[mb][reg]);
+    }
+  double e[TileW::MB][4][TileW::NB];
+#pragma unroll
+  for (int mb = 0; mb < TileW::MB; ++mb)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+      for (int nb = 0; nb < TileW::NB; ++nb) e[mb][reg][nb] = 0.0;
+  for (int b = 0; b < kmx; ++b) {
+#pragma unroll
+    for (int mb = 0; mb < TileW::MB; ++mb)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        if (b < kss[mb][reg]) {
+          const double sh = SHl[TileW::row_of(mb, reg) * SHS + b];
+          const double* wrow = Wl + (lcs[mb][reg] + b) * WLS;
+#pragma unroll
+          for (int nb = 0; nb < TileW::NB; ++nb) e[mb][reg][nb] = fma(wrow[TileW::col_of(nb)], sh, e[mb][reg][nb]);
+        }
+      }
+  }
+#pragma unroll
+  for (int mb = 0; mb < TileW::MB; ++mb)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      if (!kss[mb][reg]) continue;
+      const int c = TileW::row_of(mb, reg);
+#pragma unroll
+      for (int nb = 0; nb < TileW::NB; ++nb) {
+        const int i = TileW::col_of(nb);
+        wdst[(long)c * m_pad + i] = mu_rule(Wl[c * WLS + i], tl.acc[mb][nb][reg], e[mb][reg][nb]);
+      }
+    }
 }
+
+#define k_ahtw k_ahtw_t<0>
 
 // ---------------------------------------------------------------------------------------------
 // Repacking (compaction of live restarts) and the final-factor archive: k rows per job.

@@ -31,7 +31,8 @@ def allreduce_counts(counts, group=None):
     return counts
 
 
-def run_sharded_sweep(engine, ks, R: int, *, rank: int, world: int, counts_tensor=None, group=None, **run_kwargs):
+def run_sharded_sweep(engine, ks, R: int, *, rank: int, world: int, counts_tensor=None, group=None, reduce: bool = True,
+                      **run_kwargs):
     """Runs this rank's shard on `engine` (nmfconsensus_amd.nmf.Engine on the rank's GPU) and
     all-reduces the counts.  `counts_tensor`: a torch.int32 CUDA tensor of shape (nk, n, n) that the
     engine writes directly (device pointer) and RCCL reduces; allocated if None.
@@ -44,7 +45,7 @@ def run_sharded_sweep(engine, ks, R: int, *, rank: int, world: int, counts_tenso
     if counts_tensor is None:
         counts_tensor = torch.zeros((nk, n, n), dtype=torch.int32, device="cuda")
     res = engine.run(ks, R, job_begin=jb, job_end=je, counts_device_ptr=counts_tensor.data_ptr(), **run_kwargs)
-    if world > 1:
+    if world > 1 and reduce:
         allreduce_counts(counts_tensor, group)
     return counts_tensor, res
 

@@ -14,6 +14,21 @@ __global__ void layout_k(const double* A, const double* B, double* C) {
   for (int r = 0; r < 4; r++) C[l * 4 + r] = acc[r];
 }
 
+// Is v_mfma_f64_16x16x4_f64 bit-for-bit the k-ordered fma chain D = fma(a3,b3,fma(a2,b2,fma(a1,b1,fma(a0,b0,C))))?
+__global__ void chain_k(const double* A, const double* B, const double* C, double* D, double* Dref) {
+  int l = threadIdx.x;
+  d4 acc;
+  for (int r = 0; r < 4; ++r) acc[r] = C[((l >> 4) + 4 * r) * 16 + (l & 15)];
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(l & 15) * 4 + (l >> 4)], B[(l >> 4) * 16 + (l & 15)], acc, 0, 0, 0);
+  for (int r = 0; r < 4; ++r) {
+    const int row = (l >> 4) + 4 * r, col = l & 15;
+    D[row * 16 + col] = acc[r];
+    double s = C[row * 16 + col];
+    for (int k = 0; k < 4; ++k) s = fma(A[row * 4 + k], B[k * 16 + col], s);
+    Dref[row * 16 + col] = s;
+  }
+}
+
 template <int NACC>
 __global__ void rate_k(double* out, int iters, double seed) {
   d4 acc[NACC];
@@ -62,6 +77,25 @@ int main() {
   }
   printf("layout: row=(lane>>4)+4*reg: %s ; row=(lane>>4)*4+reg: %s\n", ok_guide ? "MATCH" : "no", ok_f32 ? "MATCH" : "no");
 
+  {
+    double hA2[64], hB2[64], hC2[256];
+    unsigned long long x = 88172645463325252ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return (double)(x >> 11) / 9007199254740992.0 * 2 - 1; };
+    int same = 0, tot = 0;
+    double *dA2, *dB2, *dC2, *dD, *dR;
+    CK(hipMalloc(&dA2, 512)); CK(hipMalloc(&dB2, 512)); CK(hipMalloc(&dC2, 2048)); CK(hipMalloc(&dD, 2048)); CK(hipMalloc(&dR, 2048));
+    for (int trial = 0; trial < 200; ++trial) {
+      for (int i = 0; i < 64; ++i) { hA2[i] = rnd() * (1 << (trial % 20)); hB2[i] = rnd() / (1 + trial % 7); }
+      for (int i = 0; i < 256; ++i) hC2[i] = rnd() * 1e3;
+      CK(hipMemcpy(dA2, hA2, 512, hipMemcpyHostToDevice)); CK(hipMemcpy(dB2, hB2, 512, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dC2, hC2, 2048, hipMemcpyHostToDevice));
+      chain_k<<<1, 64>>>(dA2, dB2, dC2, dD, dR);
+      double hD[256], hR[256];
+      CK(hipMemcpy(hD, dD, 2048, hipMemcpyDeviceToHost)); CK(hipMemcpy(hR, dR, 2048, hipMemcpyDeviceToHost));
+      for (int i = 0; i < 256; ++i) { tot++; same += (hD[i] == hR[i]); }
+    }
+    printf("f64 MFMA == k-ordered fma chain: %d / %d entries bit-identical\n", same, tot);
+  }
   double* dout; CK(hipMalloc(&dout, 1 << 24));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   int iters = 4000; float ms;
