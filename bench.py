@@ -212,6 +212,18 @@ def main():
         ach = kernels[dom]["tflops"]
         roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None, "kernels": kernels}
+        # HBM bytes per launch of the dominant kernel from the committed PMC passes
+        # (tools/profile_round.sh: FETCH_SIZE x 2 + WRITE_SIZE, full-load launches)
+        tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tp) and args.config == "C3":
+            try:
+                pm = json.load(open(tp))
+                key = "k_wta" if dom == "wta" else ("k_ahtw_t" if "k_ahtw_t" in pm else "k_ahtw")
+                if key in pm:
+                    roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
+                    roof["traffic_unit"] = "bytes per full-load launch (rocprofv3 PMC, profiles/pmc_traffic.json)"
+            except Exception as ex:
+                log(f"[bench] could not read {tp}: {ex!r}")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -280,7 +280,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   e->n_cols_pad = round_up(n, 128);    // sample tiles of W^T A
   e->ngt = (int)(e->m_pad / GT);
   // fixed gene chunks of W^T A: a function of m only, so every entry's summation order is batch-independent
-  e->kchunk = 4096;
+  e->kchunk = (int)std::min<long>(2048, e->m_pad);
   e->nsplit = (int)((e->m_pad + e->kchunk - 1) / e->kchunk);
   if (e->Acm.ensure(sizeof(double) * e->n_cols_pad * e->m_pad) || e->Arm.ensure(sizeof(double) * e->m_pad * e->n_pad)) {
     nmfc_engine_destroy(e);

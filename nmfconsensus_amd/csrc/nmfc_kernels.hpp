@@ -411,8 +411,15 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
   if (tid == 0) changed = 0;
   for (int idx = tid; idx < k * k; idx += NT) {
     const double* src = SWpart + me.sq_off + idx;
-    double sacc = src[0];
-    for (int g = 1; g < nsplit; ++g) sacc += src[(long)g * sw_total];
+    double sacc = 0.0;
+    for (int g0 = 0; g0 < nsplit; g0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = (g0 + u < nsplit) ? src[(long)(g0 + u) * sw_total] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (g0 + u < nsplit) sacc = (g0 + u == 0) ? v[u] : sacc + v[u];
+    }
     sw[(idx / k) * KMAX + (idx % k)] = sacc;
   }
   for (int idx = tid; idx < KMAX * KMAX; idx += NT) win[idx] = 0.0;
@@ -438,8 +445,16 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
       double hn = 0.0;
       if (valid) {
         const long goff = (long)(c0 + a) * g_ld + j;
-        double gsum = Gpart[goff];
-        for (int sp = 1; sp < nsplit; ++sp) gsum += Gpart[(long)sp * g_split + goff];
+        // chunk partials summed in chunk order; loads issued 8 at a time for memory-level parallelism
+        double gsum = 0.0;
+        for (int sp0 = 0; sp0 < nsplit; sp0 += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = (sp0 + u < nsplit) ? Gpart[(long)(sp0 + u) * g_split + goff] : 0.0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (sp0 + u < nsplit) gsum = (sp0 + u == 0) ? v[u] : gsum + v[u];
+        }
         double d = 0.0;
         for (int bb = 0; bb < k; ++bb) d = fma(sw[a * KMAX + bb], Hc[bb * HCH + tid], d);
         hn = mu_rule(Hc[a * HCH + tid], gsum, d);
@@ -523,19 +538,16 @@ constexpr int SHS = KMAX + 1;      // LDS row stride of the h h^T rows
 constexpr int AHTW_EPI = PANEL * WLS + PANEL * SHS;
 constexpr int AHTW_LDS = (TileW::LDS_DOUBLES > AHTW_EPI) ? TileW::LDS_DOUBLES : AHTW_EPI;
 
-// PREF selects where the W0 prefetch is issued: 0 = during the last K stage, 1 = right after the
-// prologue (kept as a template switch for tools/kbench.hip).
-template <int PREF>
-static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double* __restrict__ H, long n_pad,
-                                                       const double* __restrict__ Arm, long m_pad,
-                                                       double* __restrict__ W, const double* __restrict__ SH,
-                                                       const int* __restrict__ prb, const int* __restrict__ pre,
-                                                       const RestartInfo* __restrict__ ri,
-                                                       const ColInfo* __restrict__ ci,
-                                                       const int* __restrict__ stop_iter, int npanels, int ngt) {
-  __shared__ __attribute__((aligned(16))) double smem[AHTW_LDS];
-  __shared__ int c_lc0[PANEL], c_k[PANEL], c_act[PANEL];
-  const int item = xcd_item(blockIdx.x, npanels * ngt);
+// One (panel, gene tile) item of K3.  Returns without touching memory when the panel is idle.
+// VARIANT != 0 only in tools/kbench (cost breakdown): 1 no W0 prefetch, 2 no E, 3 no W store.
+template <int VARIANT>
+__device__ __forceinline__ void ahtw_item(int item, int iter, const double* __restrict__ H, long n_pad,
+                                          const double* __restrict__ Arm, long m_pad, double* __restrict__ W,
+                                          const double* __restrict__ SH, const int* __restrict__ prb,
+                                          const int* __restrict__ pre, const RestartInfo* __restrict__ ri,
+                                          const ColInfo* __restrict__ ci, const int* __restrict__ stop_iter,
+                                          int npanels, int ngt, double* __restrict__ smem, int* __restrict__ c_lc0,
+                                          int* __restrict__ c_k, int* __restrict__ c_act) {
   // bands of 8 panels, gene super-tiles of 8: neighbouring items share operands in L2
   int p, gt;
   {
@@ -547,7 +559,7 @@ static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double*
     const int gsz = min(SG, ngt - sg * SG);
     const int w2 = rem - sg * bp * SG;
     p = band * SP + w2 / gsz;
-    gt = sg * SG + w2 % gsz;
+    gt = ngt - 1 - (sg * SG + w2 % gsz);   // high gene tiles first: W^T A streamed them last (MALL-warm)
   }
   if (!panel_live(prb, pre, p, ri, stop_iter, iter)) return;
   const int tid = threadIdx.x;
@@ -560,11 +572,7 @@ static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double*
   const int nst = (int)(n_pad / BK);
   tl.bind(P, n_pad, Q, n_pad);
   tl.gload(0);
-  if (PREF == 1) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      wpre[j] = *reinterpret_cast<const d2*>(wsrc + (long)((tid >> 6) + 4 * j) * m_pad + (tid & 63) * 2);
-  }
+  __syncthreads();   // the previous item's epilogue is done with smem
   tl.swrite(smem);
   __syncthreads();
   for (int st = 0; st + 1 < nst; ++st) {
@@ -574,12 +582,11 @@ static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double*
     tl.swrite(smem);
     __syncthreads();
   }
-  if (PREF == 0) {
-    // last stage: no staging load is in flight, so the W0 prefetch overlaps this stage's MFMAs
+  // last stage: no staging load is in flight, so the W0 prefetch overlaps this stage's MFMAs
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      wpre[j] = *reinterpret_cast<const d2*>(wsrc + (long)((tid >> 6) + 4 * j) * m_pad + (tid & 63) * 2);
-  }
+  for (int j = 0; j < 16; ++j)
+    wpre[j] = VARIANT == 1 ? d2{1.0, 1.0}
+                           : *reinterpret_cast<const d2*>(wsrc + (long)((tid >> 6) + 4 * j) * m_pad + (tid & 63) * 2);
   tl.compute(smem);
   __syncthreads();
   // epilogue staging: W0 tile, the panel's compact h h^T blocks, per-column restart info
@@ -606,38 +613,44 @@ static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double*
   }
   __syncthreads();
   double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GT;
-  // E = W0 (h h^T) for the lane's 32 accumulator elements, b-outer so the 32 fma chains are
-  // independent (each chain still sums b = 0..k-1 in order, as the VALU reference does)
-  int lcs[TileW::MB][4], kss[TileW::MB][4];
-  int kmx = 0;
+  // E = S W0 on the MFMA pipe.  S is the panel's block-diagonal h h^T: row c holds SH_r[c - lc0][.]
+  // on its restart's columns lc0..lc0+k-1 and zeros elsewhere (all zeros for idle columns).  The
+  // f64 MFMA is a k-ordered fma chain, so E[c][i] = sum_b SH_r[c-lc0][b] W0[lc0+b][i] accumulates
+  // exactly like the VALU chain b = 0..k-1 of nmf_mu.c:202: the zero terms around the block leave
+  // the chain unchanged.  K runs only over the columns the 16 rows of a block touch.
+  const int lane = tid & 63;
+  d4 e[TileW::MB][TileW::NB];
+  int kss[TileW::MB][4];
 #pragma unroll
-  for (int mb = 0; mb < TileW::MB; ++mb)
+  for (int mb = 0; mb < TileW::MB; ++mb) {
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int c = TileW::row_of(mb, reg);
-      lcs[mb][reg] = c_lc0[c];
       kss[mb][reg] = c_act[c] ? c_k[c] : 0;
-      kmx = max(kmx, kss[mb][reg]);
     }
-  double e[TileW::MB][4][TileW::NB];
+    const int ra = mb * 16 + (lane & 15);   // MFMA A-operand row of this lane
+    const int alc = c_lc0[ra];
+    const int ak = (VARIANT == 2 || !c_act[ra]) ? 0 : c_k[ra];
+    int lo = ak ? alc : PANEL, hi = ak ? alc + ak : 0;
 #pragma unroll
-  for (int mb = 0; mb < TileW::MB; ++mb)
+    for (int off = 8; off >= 1; off >>= 1) {
+      lo = min(lo, __shfl_xor(lo, off));
+      hi = max(hi, __shfl_xor(hi, off));
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo) & ~3;
+    hi = __builtin_amdgcn_readfirstlane(hi);
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg)
+    for (int nb = 0; nb < TileW::NB; ++nb) e[mb][nb] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int kk = lo; kk < hi; kk += 4) {
+      const int cp = kk + (lane >> 4);
+      const int bb = cp - alc;
+      const double av = (bb >= 0 && bb < ak) ? SHl[ra * SHS + bb] : 0.0;
 #pragma unroll
-      for (int nb = 0; nb < TileW::NB; ++nb) e[mb][reg][nb] = 0.0;
-  for (int b = 0; b < kmx; ++b) {
-#pragma unroll
-    for (int mb = 0; mb < TileW::MB; ++mb)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        if (b < kss[mb][reg]) {
-          const double sh = SHl[TileW::row_of(mb, reg) * SHS + b];
-          const double* wrow = Wl + (lcs[mb][reg] + b) * WLS;
-#pragma unroll
-          for (int nb = 0; nb < TileW::NB; ++nb) e[mb][reg][nb] = fma(wrow[TileW::col_of(nb)], sh, e[mb][reg][nb]);
-        }
+      for (int nb = 0; nb < TileW::NB; ++nb) {
+        const double bv = cp < hi ? Wl[cp * WLS + TileW::col_of(nb)] : 0.0;
+        e[mb][nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, e[mb][nb], 0, 0, 0);
       }
+    }
   }
 #pragma unroll
   for (int mb = 0; mb < TileW::MB; ++mb)
@@ -648,9 +661,25 @@ static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double*
 #pragma unroll
       for (int nb = 0; nb < TileW::NB; ++nb) {
         const int i = TileW::col_of(nb);
-        wdst[(long)c * m_pad + i] = mu_rule(Wl[c * WLS + i], tl.acc[mb][nb][reg], e[mb][reg][nb]);
+        const double v = mu_rule(Wl[c * WLS + i], tl.acc[mb][nb][reg], e[mb][nb][reg]);
+        if (VARIANT != 3 || v == (double)iter * 1.5e300) wdst[(long)c * m_pad + i] = v;
       }
     }
+}
+
+// One item per workgroup; two workgroups share a CU (one's epilogue overlaps the other's MFMA loop).
+template <int VARIANT>
+static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double* __restrict__ H, long n_pad,
+                                                       const double* __restrict__ Arm, long m_pad,
+                                                       double* __restrict__ W, const double* __restrict__ SH,
+                                                       const int* __restrict__ prb, const int* __restrict__ pre,
+                                                       const RestartInfo* __restrict__ ri,
+                                                       const ColInfo* __restrict__ ci,
+                                                       const int* __restrict__ stop_iter, int npanels, int ngt) {
+  __shared__ __attribute__((aligned(16))) double smem[AHTW_LDS];
+  __shared__ int c_lc0[PANEL], c_k[PANEL], c_act[PANEL];
+  ahtw_item<VARIANT>(xcd_item(blockIdx.x, npanels * ngt), iter, H, n_pad, Arm, m_pad, W, SH, prb, pre, ri, ci, stop_iter,
+            npanels, ngt, smem, c_lc0, c_k, c_act);
 }
 
 #define k_ahtw k_ahtw_t<0>

@@ -103,7 +103,7 @@ int main(int argc, char** argv) {
   for (int k = 10; k >= 2; --k) ks.push_back(k);
   const long m_pad = (m + GT - 1) / GT * GT, n_pad = (n + BK - 1) / BK * BK, n_cols_pad = (n + 127) / 128 * 128;
   const int ngt = (int)(m_pad / GT);
-  const int kchunk = 4096, nsplit = (int)((m_pad + kchunk - 1) / kchunk);
+  const int kchunk = 2048, nsplit = (int)((m_pad + kchunk - 1) / kchunk);
   // packing
   std::vector<RestartInfo> ri;
   std::vector<int> prb, pre;
@@ -214,11 +214,15 @@ int main(int argc, char** argv) {
                        dci, stop, npanels, ngt);
   }, reps);
   printf("k_ahtw       %8.3f ms  %6.1f TF useful\n", t, useful / t / 1e9);
-  t = timeit([&] {
-    hipLaunchKernelGGL(k_ahtw_t<1>, dim3(npanels * ngt), dim3(NT), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SH, dprb, dpre,
-                       dri, dci, stop, npanels, ngt);
-  }, reps);
-  printf("k_ahtw pref1 %8.3f ms  %6.1f TF useful\n", t, useful / t / 1e9);
+#define AHTW_VAR(V, label)                                                                                  \
+  t = timeit([&] {                                                                                          \
+    hipLaunchKernelGGL(k_ahtw_t<V>, dim3(npanels * ngt), dim3(NT), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SH, dprb, \
+                       dpre, dri, dci, stop, npanels, ngt);                                              \
+  }, reps);                                                                                                 \
+  printf("k_ahtw %-14s %8.3f ms\n", label, t);
+  AHTW_VAR(1, "no W0 load")
+  AHTW_VAR(2, "no E")
+  AHTW_VAR(3, "no W store")
   t = timeit([&] {
     hipLaunchKernelGGL(k_hupdate, dim3(nact), dim3(NT), 0, 0, 1, 10000, 0, dri, n, n_pad, Gpart, g_ld, g_split, nsplit,
                        SWpart, sw_total, Hh, SH, stop, reason, unch, cls, 512L, nst);
