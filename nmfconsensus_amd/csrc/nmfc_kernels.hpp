@@ -217,6 +217,191 @@ struct Tile {
   }
 };
 
+// ---------------------------------------------------------------------------------------------
+// GTile: the LDS-DMA-staged MFMA tile (v2 core).  RP x RQ outputs over NW waves (WR x WC), K in
+// stages of BK2 = 16 doubles (one 128 B row per tile row per stage) in a ring of 3 LDS buffers filled
+// by buffer_load ... lds (16 B per lane, no VGPR round trip).  A stage is issued two steps ahead; each
+// step ends with ONE counted vmcnt wait + a raw s_barrier, so the next stage's DMA stays in flight
+// across it.  LDS image: row r at r*128 B, logical 16-byte slot s stored at physical slot
+// s ^ ((r >> 1) & 7) -- the swizzle is applied on the per-lane SOURCE address (the DMA destination is
+// lane-linear) and on the fragment reads; it makes the ds_read_b128 fragment reads conflict-free.
+// Canonical K order (a function of the 16-aligned K block only): MFMA j = 2*kk + sub (kk, sub in
+// {0,1}) consumes k = 8*kk + sub + 2*g for lane group g = 0..3.  Every GTile shape uses this order, so
+// results are bit-identical across tile shapes (the tail variants) and batch compositions.
+// ---------------------------------------------------------------------------------------------
+constexpr int BK2 = 16;
+constexpr int GT_NBUF = 3;
+
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, uint32_t lds_addr, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(uintptr_t)lds_addr, 16, voff,
+                                           soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void step_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int RP, int RQ, int WR, int WC, int NBUF = GT_NBUF>
+struct GTile {
+  static_assert(NBUF == 2 || NBUF == 3, "ring of 2 or 3 stages");
+  static constexpr int NW = WR * WC;
+  static constexpr int NTH = NW * 64;
+  static constexpr int STAGE_BYTES = (RP + RQ) * BK2 * 8;
+  static constexpr int LDS_BYTES = NBUF * STAGE_BYTES;
+  static constexpr int PIECES = (RP + RQ) / 8;   // 1 KiB DMA pieces (8 rows) per stage
+  static constexpr int PPW = PIECES / NW;        // pieces per wave per stage
+  static constexpr int PPW_P = RP / 8 / NW;      // of which rows of P
+  static_assert(PIECES % NW == 0 && (RP / 8) % NW == 0, "pieces must split evenly over waves");
+  static constexpr int MB = RP / WR / 16;
+  static constexpr int NB = RQ / WC / 16;
+
+  d4 acc[MB][NB];
+  __amdgpu_buffer_rsrc_t rp, rq;
+  int voff[PPW];
+
+  // P rows are K-contiguous at P + row*ldp, Q rows at Q + row*ldq (doubles)
+  __device__ __forceinline__ void bind(const double* P, long ldp, const double* Q, long ldq) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(P), 0, (int)(RP * ldp * 8), 0x00020000);
+    rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Q), 0, (int)(RQ * ldq * 8), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int piece = w + NW * i;
+      const bool isq = i >= PPW_P;
+      const int row = (isq ? piece - RP / 8 : piece) * 8 + (l >> 3);
+      const int slot = (l & 7) ^ ((row >> 1) & 7);
+      voff[i] = (int)((long)row * (isq ? ldq : ldp) * 8 + slot * 16);
+    }
+  }
+
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+  }
+
+  // DMA of the stage starting at K position k0 into the LDS buffer at byte address `buf`
+  __device__ __forceinline__ void issue(uint32_t buf, int k0) const {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const uint32_t dst = buf + (uint32_t)(w + NW * i) * 1024u;
+      lds_dma16(i >= PPW_P ? rq : rp, dst, voff[i], k0 * 8);
+    }
+  }
+
+  // byte offset of (row, logical slot) in a stage
+  __device__ __forceinline__ static uint32_t off(int row, int slot) {
+    return (uint32_t)(row * 128 + ((slot ^ ((row >> 1) & 7)) << 4));
+  }
+
+  __device__ __forceinline__ void compute(const char* __restrict__ st) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int wr = w / WC, wc = w % WC;
+    const int fr = l & 15, g = l >> 4;
+    const char* sp = st + (wr * (RP / WR) + fr) * 128;
+    const char* sq = st + RP * 128 + (wc * (RQ / WC) + fr) * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int so = ((4 * kk + g) ^ (fr >> 1)) << 4;
+      d2 a[MB], b[NB];
+#pragma unroll
+      for (int i = 0; i < MB; ++i) a[i] = *reinterpret_cast<const d2*>(sp + i * 16 * 128 + so);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) b[j] = *reinterpret_cast<const d2*>(sq + j * 16 * 128 + so);
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // the pipelined K loop over [kbeg, kend) (multiple of BK2); `extra(stage_ptr)` runs after each
+  // stage's MFMAs on the same staged data.  smem: GT_NBUF * STAGE_BYTES bytes.
+  template <class Extra>
+  __device__ __forceinline__ void run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
+                                      int kbeg, int kend, char* __restrict__ smem, Extra extra) {
+    run(P, ldp, Q, ldq, kbeg, kend, smem, extra, [] {});
+  }
+
+  // as above; `at_last()` runs at the start of the last step (no DMA in flight: a place to issue the
+  // epilogue's own global loads so that they overlap the last stage's MFMAs)
+  template <class Extra, class AtLast>
+  __device__ __forceinline__ void run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
+                                      int kbeg, int kend, char* __restrict__ smem, Extra extra, AtLast at_last) {
+    const int nst = (kend - kbeg) / BK2;
+    bind(P, ldp, Q, ldq);
+    const uint32_t base = (uint32_t)(uintptr_t)smem;
+    if constexpr (NBUF == 2) {   // one stage in flight, issued after the barrier that freed its buffer
+      issue(base, kbeg);
+      wait_vmcnt<0>();
+      step_barrier();
+      for (int s = 0; s < nst; ++s) {
+        const int b = s & 1;
+        if (s + 1 < nst) issue(base + (b ^ 1) * STAGE_BYTES, kbeg + (s + 1) * BK2);
+        const char* cur = smem + b * STAGE_BYTES;
+        if (s + 1 == nst) at_last();
+        compute(cur);
+        extra(cur);
+        if (s + 1 < nst) {
+          wait_vmcnt<0>();
+          step_barrier();
+        }
+      }
+      return;
+    }
+    issue(base, kbeg);
+    if (nst > 1) {
+      issue(base + STAGE_BYTES, kbeg + BK2);
+      wait_vmcnt<PPW>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    step_barrier();
+    int b = 0;
+    for (int s = 0; s < nst; ++s) {
+      if (s + 2 < nst) {
+        const int b2 = (b + 2 >= NBUF) ? b + 2 - NBUF : b + 2;
+        issue(base + b2 * STAGE_BYTES, kbeg + (s + 2) * BK2);
+      }
+      const char* cur = smem + b * STAGE_BYTES;
+      if (s + 1 == nst) at_last();
+      compute(cur);
+      extra(cur);
+      if (s + 1 < nst) {
+        if (s + 2 < nst)
+          wait_vmcnt<PPW>();
+        else
+          wait_vmcnt<0>();
+        step_barrier();
+      }
+      b = (b + 1 == NBUF) ? 0 : b + 1;
+    }
+  }
+
+  // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+  __device__ __forceinline__ static int row_of(int mb, int reg) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    return (w / WC) * (RP / WR) + mb * 16 + (l >> 4) + 4 * reg;
+  }
+  __device__ __forceinline__ static int col_of(int nb) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    return (w % WC) * (RQ / WC) + nb * 16 + (l & 15);
+  }
+};
+
 // Per-restart metadata.  rid is the persistent restart index (stop state, Gram/SH offsets, output
 // slot); col0 is its current first column in W/H (changes when the engine repacks live restarts).
 struct RestartInfo {
@@ -376,6 +561,121 @@ static __global__ __launch_bounds__(NT) void k_wta(const double* __restrict__ W,
         const int lcn = (my_rb[x] & 63) + fr;           // panel-local col column index
         const ColInfo cr = cp[lr];
         if (cr.k == 0 || cr.lc0 != cp[lcn].lc0 || cp[lcn].k == 0) continue;   // not the same restart
+        const int a = lr - cr.lc0, b = lcn - cr.lc0;
+        so[cr.sq_off + a * cr.k + b] = gacc[x][reg];
+        so[cr.sq_off + b * cr.k + a] = gacc[x][reg];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1 v2 "wta2": G = W^T A on the GTile core.  A tile = NPT panels (64*NPT restart columns) x RQ
+// samples; waves WR x WC.  Gram blocks (per panel: 4 diagonal + 3 straddling 16x16 blocks) are spread
+// over the ntj sample-tile workgroups of the panel group and their waves.
+// ---------------------------------------------------------------------------------------------
+template <int NPT, int RQ, int WR, int WC, int GPW>
+static __global__ __launch_bounds__(WR * WC * 64) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
+                                                              long m_pad, int ngroups, int ntj, int nsplit, int kchunk,
+                                                              const int* __restrict__ prb, const int* __restrict__ pre,
+                                                              const RestartInfo* __restrict__ ri,
+                                                              const ColInfo* __restrict__ ci,
+                                                              const int* __restrict__ stop_iter, double* __restrict__ Gpart,
+                                                              long g_ld, long g_split, double* __restrict__ SWpart,
+                                                              long sw_total) {
+  using T = GTile<64 * NPT, RQ, WR, WC>;
+  constexpr int NCAND = 7 * NPT;
+  __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES + 64];
+  int* need = reinterpret_cast<int*>(smem + T::LDS_BYTES);
+  const int nitems = nsplit * ngroups * ntj;
+  const int item = xcd_item(blockIdx.x, nitems);
+  const int t = item % ntj;
+  const int pg = (item / ntj) % ngroups;
+  const int s = item / (ntj * ngroups);
+  bool live[NPT];
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < NPT; ++q) {
+    live[q] = panel_live(prb, pre, NPT * pg + q, ri, stop_iter, 0);
+    any = any || live[q];
+  }
+  if (!any) return;
+  if (threadIdx.x < NCAND) {
+    const int q = threadIdx.x / 7, x = threadIdx.x % 7;
+    const int br = x < 4 ? x : x - 4, bc = x < 4 ? x : x - 3;
+    int nd = live[q];
+    if (nd && br != bc) {
+      const ColInfo c = ci[(long)(NPT * pg + q) * PANEL + 16 * bc];
+      nd = (c.k > 0 && c.lc0 < 16 * bc);
+    }
+    need[threadIdx.x] = nd;
+  }
+  const double* P = W + (long)pg * 64 * NPT * m_pad;
+  const double* Q = Acm + (long)t * RQ * m_pad;
+  const int kbeg = s * kchunk;
+  const int kend = (int)min((long)kbeg + kchunk, m_pad);
+  T tl;
+  tl.zero();
+  d4 gacc[GPW];
+#pragma unroll
+  for (int x = 0; x < GPW; ++x) gacc[x] = (d4){0.0, 0.0, 0.0, 0.0};
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int fr = l & 15, g = l >> 4;
+  __syncthreads();   // need[] visible (no DMA in flight yet)
+  int my_need[GPW], my_ra[GPW], my_rb[GPW];
+  bool gram = false;
+#pragma unroll
+  for (int x = 0; x < GPW; ++x) {
+    const int cand = t + ntj * (w + T::NW * x);
+    my_need[x] = 0;
+    my_ra[x] = 0;
+    my_rb[x] = 0;
+    if (cand < NCAND) {
+      const int q = cand / 7, xx = cand % 7;
+      const int br = xx < 4 ? xx : xx - 4, bc = xx < 4 ? xx : xx - 3;
+      my_need[x] = need[cand];
+      my_ra[x] = 64 * q + 16 * br;
+      my_rb[x] = 64 * q + 16 * bc;
+      gram = gram || my_need[x];
+    }
+  }
+  tl.run(P, m_pad, Q, m_pad, kbeg, kend, smem, [&](const char* stg) {
+    if (!gram) return;
+#pragma unroll
+    for (int x = 0; x < GPW; ++x) {
+      if (!my_need[x]) continue;
+      const char* pa = stg + (my_ra[x] + fr) * 128;
+      const char* pb = stg + (my_rb[x] + fr) * 128;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int so = ((4 * kk + g) ^ (fr >> 1)) << 4;
+        const d2 a = *reinterpret_cast<const d2*>(pa + so);
+        const d2 b = *reinterpret_cast<const d2*>(pb + so);
+        gacc[x] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b.x, gacc[x], 0, 0, 0);
+        gacc[x] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b.y, gacc[x], 0, 0, 0);
+      }
+    }
+  });
+  double* out = Gpart + (long)s * g_split + (long)pg * 64 * NPT * g_ld + (long)t * RQ;
+#pragma unroll
+  for (int mb = 0; mb < T::MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < T::NB; ++nb)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) out[(long)T::row_of(mb, reg) * g_ld + T::col_of(nb)] = tl.acc[mb][nb][reg];
+  if (gram) {
+    double* so = SWpart + (long)s * sw_total;
+#pragma unroll
+    for (int x = 0; x < GPW; ++x) {
+      if (!my_need[x]) continue;
+      const int pnl = my_ra[x] >> 6;
+      const ColInfo* cp = ci + (long)(NPT * pg + pnl) * PANEL;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int lr = (my_ra[x] & 63) + g + 4 * reg;
+        const int lcn = (my_rb[x] & 63) + fr;
+        const ColInfo cr = cp[lr];
+        if (cr.k == 0 || cr.lc0 != cp[lcn].lc0 || cp[lcn].k == 0) continue;
         const int a = lr - cr.lc0, b = lcn - cr.lc0;
         so[cr.sq_off + a * cr.k + b] = gacc[x][reg];
         so[cr.sq_off + b * cr.k + a] = gacc[x][reg];
@@ -683,6 +983,119 @@ static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double*
 }
 
 #define k_ahtw k_ahtw_t<0>
+
+// ---------------------------------------------------------------------------------------------
+// K3 v2 "ahtw2": F = A h^T on the GTile core (one panel x 128 genes, 4 waves 1 x 4, each wave all 64
+// panel rows x 32 genes; 72 KiB ring, two workgroups per CU).  The W update runs in the MFMA
+// accumulator layout with NO LDS staging of W0: each lane loads its own W0 entries (the D layout of
+// its F block, 128 B per 16 lanes) at the start of the last stage, and E = W0 (h h^T) is an MFMA whose
+// B operand is exactly those registers (rows 4q..4q+3 of the D layout are the B fragment of k-step q).
+// The panel's h h^T blocks and column info are staged in LDS before the main loop.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void ahtw_map(int item, int npanels, int ngt, int& p, int& gt) {
+  const int SP = 8, SG = 8;   // bands of 8 panels, gene super-tiles of 8: neighbours share operands in L2
+  const int band = item / (SP * ngt);
+  const int rem = item % (SP * ngt);
+  const int bp = min(SP, npanels - band * SP);
+  const int sg = rem / (bp * SG);
+  const int gsz = min(SG, ngt - sg * SG);
+  const int w2 = rem - sg * bp * SG;
+  p = band * SP + w2 / gsz;
+  gt = ngt - 1 - (sg * SG + w2 % gsz);   // high gene tiles first: W^T A streamed them last
+}
+
+using TileW2 = GTile<64, 128, 1, 4, 2>;
+constexpr int AHTW2_SH = TileW2::LDS_BYTES;                    // h h^T rows: 64 x AHTW2_SHS doubles
+constexpr int AHTW2_SHS = KMAX + 1;                             // LDS row stride of the h h^T rows
+constexpr int AHTW2_CI = AHTW2_SH + PANEL * AHTW2_SHS * 8;     // c_lc0 / c_k / c_act: 3 x 64 ints
+constexpr int AHTW2_LDS = AHTW2_CI + 3 * PANEL * 4;
+
+template <int VARIANT>
+static __global__ __launch_bounds__(256, 2) void k_ahtw2(int iter, const double* __restrict__ H, long n_pad,
+                                                         const double* __restrict__ Arm, long m_pad,
+                                                         double* __restrict__ W, const double* __restrict__ SH,
+                                                         const int* __restrict__ prb, const int* __restrict__ pre,
+                                                         const RestartInfo* __restrict__ ri,
+                                                         const ColInfo* __restrict__ ci,
+                                                         const int* __restrict__ stop_iter, int npanels, int ngt) {
+  __shared__ __attribute__((aligned(1024))) char smem[AHTW2_LDS];
+  double* SHl = reinterpret_cast<double*>(smem + AHTW2_SH);
+  int* c_lc0 = reinterpret_cast<int*>(smem + AHTW2_CI);
+  int* c_k = c_lc0 + PANEL;
+  int* c_act = c_k + PANEL;
+  int p, gt;
+  ahtw_map(xcd_item(blockIdx.x, npanels * ngt), npanels, ngt, p, gt);
+  if (!panel_live(prb, pre, p, ri, stop_iter, iter)) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  {   // the panel's h h^T blocks (row c = panel column, AHTW2_SHS doubles per row) and column info;
+      // entry (c, b) per thread, all loads independent
+#pragma unroll
+    for (int j = 0; j < PANEL * KMAX / 256; ++j) {
+      const int idx = tid + 256 * j, c = idx >> 4, b = idx & 15;
+      const ColInfo cc = ci[(long)p * PANEL + c];
+      if (b < cc.k) SHl[c * AHTW2_SHS + b] = SH[cc.sq_off + (c - cc.lc0) * cc.k + b];
+      if (b == 0) {
+        c_lc0[c] = cc.lc0;
+        c_k[c] = cc.k;
+        c_act[c] = cc.k > 0 ? (stop_iter[cc.rid] == 0 || stop_iter[cc.rid] == iter) : 0;
+      }
+    }
+  }
+  // (the ring prologue's barrier publishes SHl / c_* to the workgroup)
+  TileW2 tl;
+  tl.zero();
+  const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GT + 32 * w + (lane & 15);
+  double w0[TileW2::MB][TileW2::NB][4];
+  tl.run(H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GT * n_pad, n_pad, 0, (int)n_pad, smem,
+         [](const char*) {}, [&] {
+#pragma unroll
+           for (int mb = 0; mb < TileW2::MB; ++mb)
+#pragma unroll
+             for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+               for (int nb = 0; nb < TileW2::NB; ++nb)
+                 w0[mb][nb][reg] = VARIANT == 1 ? 1.0 : wsrc[(long)(16 * mb + (lane >> 4) + 4 * reg) * m_pad + 16 * nb];
+         });
+  double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GT + 32 * w + (lane & 15);
+#pragma unroll
+  for (int mb = 0; mb < TileW2::MB; ++mb) {
+    // E rows 16*mb .. +15 = sum over the restart's columns b of S[c][b] * W0[b][i]; K runs over the
+    // 4-column groups q the block's restarts touch (wave-uniform range)
+    const int ra = 16 * mb + (lane & 15);
+    const int alc = c_lc0[ra];
+    const int ak = (VARIANT == 2 || !c_act[ra]) ? 0 : c_k[ra];
+    int lo = ak ? alc : PANEL, hi = ak ? alc + ak : 0;
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) {
+      lo = min(lo, __shfl_xor(lo, off));
+      hi = max(hi, __shfl_xor(hi, off));
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    d4 e[TileW2::NB];
+#pragma unroll
+    for (int nb = 0; nb < TileW2::NB; ++nb) e[nb] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (4 * q + 3 < lo || 4 * q >= hi) continue;   // wave-uniform
+      const int bb = 4 * q + (lane >> 4) - alc;
+      const double av = (bb >= 0 && bb < ak) ? SHl[ra * AHTW2_SHS + bb] : 0.0;
+#pragma unroll
+      for (int nb = 0; nb < TileW2::NB; ++nb)
+        e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, w0[q >> 2][nb][q & 3], e[nb], 0, 0, 0);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int c = 16 * mb + (lane >> 4) + 4 * reg;
+      if (!c_act[c]) continue;
+#pragma unroll
+      for (int nb = 0; nb < TileW2::NB; ++nb) {
+        const double v = mu_rule(w0[mb][nb][reg], tl.acc[mb][nb][reg], e[nb][reg]);
+        if (VARIANT != 3 || v == (double)iter * 1.5e300) wdst[(long)c * m_pad + 16 * nb] = v;
+      }
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------------------------
 // Repacking (compaction of live restarts) and the final-factor archive: k rows per job.

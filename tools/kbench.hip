@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <vector>
 
 #include "../nmfconsensus_amd/csrc/nmfc_kernels.hpp"
@@ -124,7 +125,7 @@ int main(int argc, char** argv) {
       useful += 2.0 * m * n * k + 2.0 * m * k * k;
     }
   int npanels = np + 1;
-  if (npanels & 1) {
+  while (npanels & 3) {   // multiple of 4 (k_wta2 panel quads)
     prb.push_back((int)ri.size());
     pre.push_back((int)ri.size());
     ++npanels;
@@ -186,6 +187,32 @@ int main(int argc, char** argv) {
   printf("k_wta        %8.3f ms  %6.1f TF useful  %6.1f TF executed\n", t, useful / t / 1e9,
          2.0 * cols * m_pad * n_cols_pad / t / 1e9);
   {
+    const size_t gn = (size_t)nsplit * cols * n_cols_pad, sn = (size_t)nsplit * sw_total;
+    std::vector<double> g1(gn), g2(gn), s1(sn), s2(sn);
+    CK(hipMemcpy(g1.data(), Gpart, gn * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(s1.data(), SWpart, sn * 8, hipMemcpyDeviceToHost));
+    CK(hipMemset(Gpart, 0, gn * 8));
+    CK(hipMemset(SWpart, 0, sn * 8));
+    const int ngroups = npanels / 4;
+    auto kw2 = [&] {
+      hipLaunchKernelGGL((k_wta2<4, 128, 4, 2, 1>), dim3(nsplit * ngroups * ntj), dim3(512), 0, 0, W, Acm, m_pad, ngroups, ntj,
+                         nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, sw_total);
+    };
+    kw2();
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(g2.data(), Gpart, gn * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(s2.data(), SWpart, sn * 8, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0, sd = 0, sx = 0;
+    for (size_t i = 0; i < gn; ++i) { md = std::max(md, std::fabs(g1[i] - g2[i])); mx = std::max(mx, std::fabs(g1[i])); }
+    for (size_t i = 0; i < sn; ++i) { sd = std::max(sd, std::fabs(s1[i] - s2[i])); sx = std::max(sx, std::fabs(s1[i])); }
+    printf("wta2 vs wta: G max|d| %.3e (max %.3e)  Gram max|d| %.3e (max %.3e)\n", md, mx, sd, sx);
+    for (int rep = 0; rep < 3; ++rep) {
+      t = timeit(kw2, reps);
+      printf("k_wta2 256x128 8w  %8.3f ms  %6.1f TF useful  %6.1f TF executed\n", t, useful / t / 1e9,
+             2.0 * cols * m_pad * n_cols_pad / t / 1e9);
+    }
+  }
+  {
     const double ex = 2.0 * cols * m_pad * n_cols_pad;
     t = timeit([&] {
       hipLaunchKernelGGL(v_wta<0>, dim3(nsplit * npairs * ntj), dim3(NT), 0, 0, W, Acm, m_pad, npairs, ntj, nsplit,
@@ -214,6 +241,45 @@ int main(int argc, char** argv) {
                        dci, stop, npanels, ngt);
   }, reps);
   printf("k_ahtw       %8.3f ms  %6.1f TF useful\n", t, useful / t / 1e9);
+  {
+    // parity of ahtw2 vs ahtw from the same W0 (one launch each), then timing
+    double* W2;
+    const size_t wn = (size_t)cols * m_pad;
+    CK(hipMalloc(&W2, wn * 8));
+    std::vector<double> h(wn);
+    for (size_t i = 0; i < wn; ++i) h[i] = 0.25 + (double)((i * 2654435761u) % 1000) / 1000.0;
+    CK(hipMemcpy(W, h.data(), wn * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(W2, h.data(), wn * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_ahtw, dim3(npanels * ngt), dim3(NT), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SH, dprb, dpre, dri,
+                       dci, stop, npanels, ngt);
+    hipLaunchKernelGGL(k_ahtw2<0>, dim3(npanels * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm, m_pad, W2, SH, dprb, dpre, dri,
+                       dci, stop, npanels, ngt);
+    CK(hipDeviceSynchronize());
+    std::vector<double> a1(wn), a2(wn);
+    CK(hipMemcpy(a1.data(), W, wn * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(a2.data(), W2, wn * 8, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0;
+    size_t nbad = 0;
+    for (size_t i = 0; i < wn; ++i) {
+      const double d = std::fabs(a1[i] - a2[i]);
+      md = std::max(md, d / std::max(std::fabs(a1[i]), 1e-300));
+      mx = std::max(mx, std::fabs(a1[i]));
+      nbad += d > 1e-12 * std::fabs(a1[i]);
+    }
+    printf("ahtw2 vs ahtw: W max rel diff %.3e (max %.3e), %zu entries off by >1e-12\n", md, mx, nbad);
+    CK(hipFree(W2));
+#define AHTW2_VAR(V, label)                                                                                  \
+    t = timeit([&] {                                                                                        \
+      hipLaunchKernelGGL(k_ahtw2<V>, dim3(npanels * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SH, dprb, \
+                         dpre, dri, dci, stop, npanels, ngt);                                               \
+    }, reps);                                                                                               \
+    printf("k_ahtw2 %-14s %8.3f ms  %6.1f TF useful\n", label, t, useful / t / 1e9);
+    AHTW2_VAR(0, "")
+    AHTW2_VAR(0, "")
+    AHTW2_VAR(1, "no W0 load")
+    AHTW2_VAR(2, "no E")
+    AHTW2_VAR(3, "no W store")
+  }
 #define AHTW_VAR(V, label)                                                                                  \
   t = timeit([&] {                                                                                          \
     hipLaunchKernelGGL(k_ahtw_t<V>, dim3(npanels * ngt), dim3(NT), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SH, dprb, \
