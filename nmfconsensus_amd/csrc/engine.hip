@@ -113,7 +113,8 @@ std::vector<uint32_t> make_jump_table(int nchunks) {
 enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID_N = 5 };
 
 // Packing of a restart list into 64-column panels (sequential fill, k-descending order given);
-// panel count rounded up to an even number (the W^T A tile spans a panel pair).
+// panel count rounded up to a multiple of WTA_NPT (the large W^T A tile spans that many panels).
+constexpr int WTA_NPT = 4;
 struct Packing {
   std::vector<RestartInfo> ri;   // active list, panel-contiguous
   std::vector<int> prb, pre;     // per panel: [begin, end) in ri
@@ -138,15 +139,15 @@ Packing pack(const std::vector<RestartInfo>& in) {
     pk.pre[np] = (int)q + 1;
   }
   pk.npanels = np + 1;
-  if (pk.npanels & 1) {   // empty partner panel
+  if (pk.npanels == 0) {
+    pk.npanels = 1;
+    pk.prb = {0};
+    pk.pre = {0};
+  }
+  while (pk.npanels % WTA_NPT) {   // empty panels complete the last W^T A panel group
     pk.prb.push_back((int)in.size());
     pk.pre.push_back((int)in.size());
     ++pk.npanels;
-  }
-  if (pk.npanels == 0) {
-    pk.npanels = 2;
-    pk.prb = {0, 0};
-    pk.pre = {0, 0};
   }
   pk.ci.assign((size_t)pk.npanels * PANEL, ColInfo{0, 0, 0, 0});
   for (const RestartInfo& r : pk.ri)
@@ -162,6 +163,7 @@ struct nmfc_engine {
   int m = 0, n = 0;
   long m_pad = 0, n_pad = 0, n_cols_pad = 0;
   int kchunk = 0, nsplit = 0, ngt = 0;
+  int ncu = 256;   // compute units (grid-size heuristics only)
   DevBuf Acm, Arm;
   // per-run buffers (grow-only)
   DevBuf W[2], H[2], Gpart, SWpart, SH, Hfin, Wfin;
@@ -271,6 +273,10 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
     if ((err = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", err);
   }
   if ((err = hipGetDevice(&e->dev)) != hipSuccess) return fail("hipGetDevice", err);
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev) == hipSuccess && ncu > 0) e->ncu = ncu;
+  }
   if ((err = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", err);
   if ((err = hipHostMalloc((void**)&e->h_stopped, 2 * sizeof(int), 0)) != hipSuccess) return fail("hipHostMalloc", err);
   e->m = m;
@@ -543,18 +549,31 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   for (;;) {
     if (it < opts.maxiter) {
       const int chunk = std::min(opts.check_every, opts.maxiter - it);
-      const int npairs = pk.npanels / 2;
-      const int grid_wta = e->nsplit * npairs * ntj;
+      const bool wta_big = (long)e->nsplit * (pk.npanels / WTA_NPT) * ntj >= 2L * e->ncu;
       const int grid_ahtw = pk.npanels * e->ngt;
       for (int c = 1; c <= chunk; ++c) {
         const int iter = it + c;
         {
+          // W^T A on the GTile core: 4-panel x 128-sample tiles (8 waves) while the grid fills the chip
+          // at least twice, else 1-panel x 64-sample tiles (4 waves).  Both accumulate every entry in
+          // the same canonical K order, so the switch never changes a bit.
           TimedLaunch tl(e, KID_WTA);
-          auto kw = (ntj >= 4) ? k_wta<1, true> : (ntj >= 2) ? k_wta<2, false> : k_wta<4, false>;
-          hipLaunchKernelGGL(kw, dim3(grid_wta), dim3(NT), 0, st, e->W[cur].as<double>(), e->Acm.as<double>(),
-                             e->m_pad, npairs, ntj, e->nsplit, e->kchunk, e->prb.as<int>(), e->pre.as<int>(),
-                             e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(),
-                             e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
+          if (wta_big) {
+            const int ng = pk.npanels / WTA_NPT;
+            auto kw = (ntj >= 4) ? k_wta2<WTA_NPT, 128, 4, 2, 1> : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2>
+                                                                            : k_wta2<WTA_NPT, 128, 4, 2, 4>;
+            hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
+                               e->Acm.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
+                               e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
+                               e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
+                               sw_total);
+          } else {
+            hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1>), dim3(e->nsplit * pk.npanels * 2 * ntj), dim3(256), 0, st,
+                               e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, pk.npanels, 2 * ntj, e->nsplit,
+                               e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
+                               e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
+                               e->SWpart.as<double>(), sw_total);
+          }
         }
         {
           TimedLaunch tl(e, KID_HUPD);

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace nmfc {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -338,7 +340,9 @@ struct GTile {
 
   // as above; `at_last()` runs at the start of the last step (no DMA in flight: a place to issue the
   // epilogue's own global loads so that they overlap the last stage's MFMAs)
-  template <class Extra, class AtLast>
+  // NBUF == 2: `at_last()` runs right after the last DMA issue and may issue XL vector-memory
+  // operations of its own; the one wait that follows leaves those XL in flight.
+  template <int XL = 0, class Extra, class AtLast>
   __device__ __forceinline__ void run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
                                       int kbeg, int kend, char* __restrict__ smem, Extra extra, AtLast at_last) {
     const int nst = (kend - kbeg) / BK2;
@@ -348,15 +352,21 @@ struct GTile {
       issue(base, kbeg);
       wait_vmcnt<0>();
       step_barrier();
+      if (nst == 1) at_last();
       for (int s = 0; s < nst; ++s) {
         const int b = s & 1;
-        if (s + 1 < nst) issue(base + (b ^ 1) * STAGE_BYTES, kbeg + (s + 1) * BK2);
+        if (s + 1 < nst) {
+          issue(base + (b ^ 1) * STAGE_BYTES, kbeg + (s + 1) * BK2);
+          if (s + 2 == nst) at_last();
+        }
         const char* cur = smem + b * STAGE_BYTES;
-        if (s + 1 == nst) at_last();
         compute(cur);
         extra(cur);
         if (s + 1 < nst) {
-          wait_vmcnt<0>();
+          if (s + 2 == nst)
+            wait_vmcnt<XL>();
+          else
+            wait_vmcnt<0>();
           step_barrier();
         }
       }
@@ -1010,7 +1020,13 @@ constexpr int AHTW2_SHS = KMAX + 1;                             // LDS row strid
 constexpr int AHTW2_CI = AHTW2_SH + PANEL * AHTW2_SHS * 8;     // c_lc0 / c_k / c_act: 3 x 64 ints
 constexpr int AHTW2_LDS = AHTW2_CI + 3 * PANEL * 4;
 
-template <int VARIANT>
+// MAIN = 0: GTile 2-stage DMA ring main loop; MAIN = 1: the register-prefetch Tile (TileW) main loop
+// (single 48 KiB stage).  Both keep two workgroups per CU.
+constexpr int AHTW3_SH = TileW::LDS_DOUBLES * 8;
+constexpr int AHTW3_CI = AHTW3_SH + PANEL * AHTW2_SHS * 8;
+constexpr int AHTW3_LDS = AHTW3_CI + 3 * PANEL * 4;
+
+template <int VARIANT, int MAIN = 0>
 static __global__ __launch_bounds__(256, 2) void k_ahtw2(int iter, const double* __restrict__ H, long n_pad,
                                                          const double* __restrict__ Arm, long m_pad,
                                                          double* __restrict__ W, const double* __restrict__ SH,
@@ -1018,9 +1034,9 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw2(int iter, const double*
                                                          const RestartInfo* __restrict__ ri,
                                                          const ColInfo* __restrict__ ci,
                                                          const int* __restrict__ stop_iter, int npanels, int ngt) {
-  __shared__ __attribute__((aligned(1024))) char smem[AHTW2_LDS];
-  double* SHl = reinterpret_cast<double*>(smem + AHTW2_SH);
-  int* c_lc0 = reinterpret_cast<int*>(smem + AHTW2_CI);
+  __shared__ __attribute__((aligned(1024))) char smem[MAIN ? AHTW3_LDS : AHTW2_LDS];
+  double* SHl = reinterpret_cast<double*>(smem + (MAIN ? AHTW3_SH : AHTW2_SH));
+  int* c_lc0 = reinterpret_cast<int*>(smem + (MAIN ? AHTW3_CI : AHTW2_CI));
   int* c_k = c_lc0 + PANEL;
   int* c_act = c_k + PANEL;
   int p, gt;
@@ -1042,28 +1058,55 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw2(int iter, const double*
     }
   }
   // (the ring prologue's barrier publishes SHl / c_* to the workgroup)
-  TileW2 tl;
+  using TT = std::conditional_t<MAIN == 1, TileW, TileW2>;
+  TT tl;
   tl.zero();
   const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GT + 32 * w + (lane & 15);
-  double w0[TileW2::MB][TileW2::NB][4];
-  tl.run(H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GT * n_pad, n_pad, 0, (int)n_pad, smem,
-         [](const char*) {}, [&] {
+  double w0[TT::MB][TT::NB][4];
+  auto load_w0 = [&] {
 #pragma unroll
-           for (int mb = 0; mb < TileW2::MB; ++mb)
+    for (int mb = 0; mb < TT::MB; ++mb)
 #pragma unroll
-             for (int reg = 0; reg < 4; ++reg)
+      for (int reg = 0; reg < 4; ++reg)
 #pragma unroll
-               for (int nb = 0; nb < TileW2::NB; ++nb)
-                 w0[mb][nb][reg] = VARIANT == 1 ? 1.0 : wsrc[(long)(16 * mb + (lane >> 4) + 4 * reg) * m_pad + 16 * nb];
-         });
+        for (int nb = 0; nb < TT::NB; ++nb)
+          w0[mb][nb][reg] = (VARIANT == 1 || VARIANT == 4) ? 1.0 : wsrc[(long)(16 * mb + (lane >> 4) + 4 * reg) * m_pad + 16 * nb];
+  };
+  const double* P = H + (long)p * PANEL * n_pad;
+  const double* Q = Arm + (long)gt * GT * n_pad;
+  if constexpr (MAIN == 0) {
+    tl.template run<TT::MB * TT::NB * 4>(P, n_pad, Q, n_pad, 0, (int)n_pad, smem, [](const char*) {}, load_w0);
+  } else {
+    double* st = reinterpret_cast<double*>(smem);
+    const int nst = (int)(n_pad / BK);
+    tl.bind(P, n_pad, Q, n_pad);
+    tl.gload(0);
+    if (nst == 1) load_w0();
+    __syncthreads();   // SHl / c_* staged
+    tl.swrite(st);
+    __syncthreads();
+    for (int s2 = 0; s2 < nst; ++s2) {
+      const bool more = s2 + 1 < nst;
+      if (more) {
+        tl.gload((s2 + 1) * BK);
+        if (s2 + 2 == nst) load_w0();   // after the last staging load: the epilogue's W0 overlaps 2 stages
+      }
+      tl.compute(st);
+      __syncthreads();
+      if (more) {
+        tl.swrite(st);
+        __syncthreads();
+      }
+    }
+  }
   double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GT + 32 * w + (lane & 15);
 #pragma unroll
-  for (int mb = 0; mb < TileW2::MB; ++mb) {
+  for (int mb = 0; mb < TT::MB; ++mb) {
     // E rows 16*mb .. +15 = sum over the restart's columns b of S[c][b] * W0[b][i]; K runs over the
     // 4-column groups q the block's restarts touch (wave-uniform range)
     const int ra = 16 * mb + (lane & 15);
     const int alc = c_lc0[ra];
-    const int ak = (VARIANT == 2 || !c_act[ra]) ? 0 : c_k[ra];
+    const int ak = (VARIANT == 2 || VARIANT == 4 || !c_act[ra]) ? 0 : c_k[ra];
     int lo = ak ? alc : PANEL, hi = ak ? alc + ak : 0;
 #pragma unroll
     for (int off = 8; off >= 1; off >>= 1) {
@@ -1072,16 +1115,16 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw2(int iter, const double*
     }
     lo = __builtin_amdgcn_readfirstlane(lo);
     hi = __builtin_amdgcn_readfirstlane(hi);
-    d4 e[TileW2::NB];
+    d4 e[TT::NB];
 #pragma unroll
-    for (int nb = 0; nb < TileW2::NB; ++nb) e[nb] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int nb = 0; nb < TT::NB; ++nb) e[nb] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       if (4 * q + 3 < lo || 4 * q >= hi) continue;   // wave-uniform
       const int bb = 4 * q + (lane >> 4) - alc;
       const double av = (bb >= 0 && bb < ak) ? SHl[ra * AHTW2_SHS + bb] : 0.0;
 #pragma unroll
-      for (int nb = 0; nb < TileW2::NB; ++nb)
+      for (int nb = 0; nb < TT::NB; ++nb)
         e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, w0[q >> 2][nb][q & 3], e[nb], 0, 0, 0);
     }
 #pragma unroll
@@ -1089,8 +1132,8 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw2(int iter, const double*
       const int c = 16 * mb + (lane >> 4) + 4 * reg;
       if (!c_act[c]) continue;
 #pragma unroll
-      for (int nb = 0; nb < TileW2::NB; ++nb) {
-        const double v = mu_rule(w0[mb][nb][reg], tl.acc[mb][nb][reg], e[nb][reg]);
+      for (int nb = 0; nb < TT::NB; ++nb) {
+        const double v = VARIANT == 4 ? tl.acc[mb][nb][reg] : mu_rule(w0[mb][nb][reg], tl.acc[mb][nb][reg], e[nb][reg]);
         if (VARIANT != 3 || v == (double)iter * 1.5e300) wdst[(long)c * m_pad + 16 * nb] = v;
       }
     }

@@ -252,7 +252,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(W2, h.data(), wn * 8, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_ahtw, dim3(npanels * ngt), dim3(NT), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SH, dprb, dpre, dri,
                        dci, stop, npanels, ngt);
-    hipLaunchKernelGGL(k_ahtw2<0>, dim3(npanels * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm, m_pad, W2, SH, dprb, dpre, dri,
+    hipLaunchKernelGGL((k_ahtw2<0, 1>), dim3(npanels * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm, m_pad, W2, SH, dprb, dpre, dri,
                        dci, stop, npanels, ngt);
     CK(hipDeviceSynchronize());
     std::vector<double> a1(wn), a2(wn);
@@ -279,6 +279,18 @@ int main(int argc, char** argv) {
     AHTW2_VAR(1, "no W0 load")
     AHTW2_VAR(2, "no E")
     AHTW2_VAR(3, "no W store")
+    AHTW2_VAR(4, "main only")
+#define AHTW3_VAR(V, label)                                                                                  \
+    t = timeit([&] {                                                                                        \
+      hipLaunchKernelGGL((k_ahtw2<V, 1>), dim3(npanels * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SH, dprb, \
+                         dpre, dri, dci, stop, npanels, ngt);                                               \
+    }, reps);                                                                                               \
+    printf("k_ahtw3 %-14s %8.3f ms  %6.1f TF useful\n", label, t, useful / t / 1e9);
+    AHTW3_VAR(0, "")
+    AHTW3_VAR(0, "")
+    AHTW3_VAR(1, "no W0 load")
+    AHTW3_VAR(2, "no E")
+    AHTW3_VAR(4, "main only")
   }
 #define AHTW_VAR(V, label)                                                                                  \
   t = timeit([&] {                                                                                          \
