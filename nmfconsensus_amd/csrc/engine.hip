@@ -4,10 +4,10 @@
 // (libnmf/nmf_mu.c:167-293) and the consensus reduction (nmf.r:121-144) with one batched sweep on
 // one MI355X: all (k, restart) jobs of a shard are packed into 64-column panels of a stacked W/H,
 // and every MU iteration is three launches on one HIP stream:
-//   k_wta     G = W^T A                                          (fp64 MFMA, fixed gene chunks)
-//   k_wta     also the restart-diagonal blocks of W^T W (nmf_mu.c:176) from the same staged W
+//   k_wta2    G = W^T A                                          (fp64 MFMA, fixed gene chunks)
+//   k_wta2    also the restart-diagonal blocks of W^T W (nmf_mu.c:176) from the same staged W
 //   k_hupdate W^T W from the chunk partials, H update, H H^T, stability check (one workgroup per restart)
-//   k_ahtw    A h^T fused with W0 (h h^T) and the W update (fp64 MFMA)
+//   k_ahtw4   A h^T fused with W0 (h h^T) and the W update (fp64 MFMA)
 // Restarts that stop are archived and the live ones repacked into fewer panels as the sweep goes.
 #include <hip/hip_runtime.h>
 
@@ -166,7 +166,7 @@ struct nmfc_engine {
   int ncu = 256;   // compute units (grid-size heuristics only)
   DevBuf Acm, Arm;
   // per-run buffers (grow-only)
-  DevBuf W[2], H[2], Gpart, SWpart, SH, Hfin, Wfin;
+  DevBuf W[2], H[2], Gpart, SWpart, SH, SHP, colact, Hfin, Wfin;
   DevBuf rinfo, stop_iter, stop_reason, unchanged, classes, n_stopped;
   DevBuf prb, pre, colinfo, moves, finfo;
   DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp;
@@ -320,7 +320,8 @@ void nmfc_engine_destroy(nmfc_engine* e) {
   drain_timing(e);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
   DevBuf* bufs[] = {&e->Acm,       &e->Arm,       &e->W[0],      &e->W[1],     &e->H[0],       &e->H[1],
-                    &e->Gpart,     &e->SWpart,    &e->SH,        &e->Hfin,     &e->Wfin,       &e->rinfo,
+                    &e->Gpart,     &e->SWpart,    &e->SH,        &e->SHP,      &e->colact,     &e->Hfin,
+                    &e->Wfin,      &e->rinfo,
                     &e->stop_iter, &e->stop_reason, &e->unchanged, &e->classes, &e->n_stopped, &e->prb,
                     &e->pre,       &e->colinfo,   &e->moves,     &e->finfo,     &e->initjobs, &e->chunk_job,  &e->chunk_idx,
                     &e->jump,      &e->labels,    &e->slot,      &e->grp_begin, &e->grp_list,  &e->counts_tmp,
@@ -424,6 +425,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       e->W[1].ensure(sizeof(double) * cap_cols * e->m_pad) || e->H[1].ensure(sizeof(double) * cap_cols * e->n_pad) ||
       e->Gpart.ensure(sizeof(double) * g_split * e->nsplit) || e->SWpart.ensure(sizeof(double) * sw_total * e->nsplit) ||
       e->SH.ensure(sizeof(double) * sw_total) || e->Hfin.ensure(sizeof(double) * fin_rows * e->n_pad) ||
+      e->SHP.ensure(sizeof(double) * cap_cols * KMAX) || e->colact.ensure(sizeof(int) * cap_cols) ||
       (want_w && e->Wfin.ensure(sizeof(double) * fin_rows * e->m_pad)) || e->rinfo.ensure(sizeof(RestartInfo) * nj) ||
       e->finfo.ensure(sizeof(RestartInfo) * nj) || e->stop_iter.ensure(sizeof(int) * nj) ||
       e->stop_reason.ensure(sizeof(int) * nj) || e->unchanged.ensure(sizeof(int) * nj) ||
@@ -450,6 +452,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   HCHECK(hipMemsetAsync(e->unchanged.p, 0, sizeof(int) * nj, st));
   HCHECK(hipMemsetAsync(e->classes.p, 0, sizeof(int) * nj * cls_ld, st));   // nmf_mu.c:132 zero start
   HCHECK(hipMemsetAsync(e->n_stopped.p, 0, sizeof(int), st));
+  HCHECK(hipMemsetAsync(e->colact.p, 0, sizeof(int) * cap_cols, st));
   HCHECK(hipMemsetAsync(e->W[0].p, 0, sizeof(double) * cap_cols * e->m_pad, st));
   HCHECK(hipMemsetAsync(e->H[0].p, 0, sizeof(double) * cap_cols * e->n_pad, st));
   HCHECK(hipMemsetAsync(e->W[1].p, 0, sizeof(double) * cap_cols * e->m_pad, st));
@@ -581,14 +584,14 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                              e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, e->nsplit,
                              e->SWpart.as<double>(), sw_total, e->H[cur].as<double>(), e->SH.as<double>(),
                              e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->unchanged.as<int>(),
-                             e->classes.as<int>(), cls_ld, e->n_stopped.as<int>());
+                             e->classes.as<int>(), cls_ld, e->n_stopped.as<int>(), e->SHP.as<double>(),
+                             e->colact.as<int>());
         }
         {
           TimedLaunch tl(e, KID_AHTW);
-          hipLaunchKernelGGL(k_ahtw, dim3(grid_ahtw), dim3(NT), 0, st, iter, e->H[cur].as<double>(), e->n_pad,
-                             e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(), e->SH.as<double>(),
-                             e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
-                             e->stop_iter.as<int>(), pk.npanels, e->ngt);
+          hipLaunchKernelGGL(k_ahtw4<0>, dim3(grid_ahtw), dim3(256), 0, st, iter, e->H[cur].as<double>(), e->n_pad,
+                             e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(), e->SHP.as<double>(),
+                             e->colinfo.as<ColInfo>(), e->colact.as<int>(), pk.npanels, e->ngt);
         }
       }
       HCHECK(hipGetLastError());

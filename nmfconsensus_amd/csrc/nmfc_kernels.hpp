@@ -338,18 +338,30 @@ struct GTile {
     run(P, ldp, Q, ldq, kbeg, kend, smem, extra, [] {});
   }
 
-  // as above; `at_last()` runs at the start of the last step (no DMA in flight: a place to issue the
-  // epilogue's own global loads so that they overlap the last stage's MFMAs)
+  // as above with `at_last()`: a place to issue the epilogue's own XL global loads early (see below)
   // NBUF == 2: `at_last()` runs right after the last DMA issue and may issue XL vector-memory
   // operations of its own; the one wait that follows leaves those XL in flight.
   template <int XL = 0, class Extra, class AtLast>
   __device__ __forceinline__ void run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
                                       int kbeg, int kend, char* __restrict__ smem, Extra extra, AtLast at_last) {
+    (void)run<XL>(P, ldp, Q, ldq, kbeg, kend, smem, [] { return true; }, extra, at_last);
+  }
+
+  // with `pre()`: runs right after the prologue's first DMA issue, so the workgroup's own setup loads
+  // overlap the first stages' latency; returning false abandons the tile (the DMA is drained first)
+  // and run returns false.  All waves must return the same answer.
+  template <int XL = 0, class Pre, class Extra, class AtLast>
+  __device__ __forceinline__ bool run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
+                                      int kbeg, int kend, char* __restrict__ smem, Pre pre, Extra extra, AtLast at_last) {
     const int nst = (kend - kbeg) / BK2;
     bind(P, ldp, Q, ldq);
     const uint32_t base = (uint32_t)(uintptr_t)smem;
     if constexpr (NBUF == 2) {   // one stage in flight, issued after the barrier that freed its buffer
       issue(base, kbeg);
+      if (!pre()) {
+        wait_vmcnt<0>();
+        return false;
+      }
       wait_vmcnt<0>();
       step_barrier();
       if (nst == 1) at_last();
@@ -370,14 +382,28 @@ struct GTile {
           step_barrier();
         }
       }
-      return;
+      return true;
     }
+    // NBUF == 3: `at_last()` runs right after the LAST DMA issue (two steps before the end) and may
+    // issue XL vector-memory operations; every later wait leaves those XL in flight.
     issue(base, kbeg);
-    if (nst > 1) {
-      issue(base + STAGE_BYTES, kbeg + BK2);
-      wait_vmcnt<PPW>();
-    } else {
+    bool xl = false;
+    if (nst > 1) issue(base + STAGE_BYTES, kbeg + BK2);
+    if (!pre()) {
       wait_vmcnt<0>();
+      return false;
+    }
+    if (nst <= 2) {
+      at_last();
+      xl = true;
+    }
+    if (nst > 1) {
+      if (xl)
+        wait_vmcnt<PPW + XL>();
+      else
+        wait_vmcnt<PPW>();
+    } else {
+      wait_vmcnt<XL>();
     }
     step_barrier();
     int b = 0;
@@ -385,20 +411,31 @@ struct GTile {
       if (s + 2 < nst) {
         const int b2 = (b + 2 >= NBUF) ? b + 2 - NBUF : b + 2;
         issue(base + b2 * STAGE_BYTES, kbeg + (s + 2) * BK2);
+        if (s + 3 == nst) {
+          at_last();
+          xl = true;
+        }
       }
       const char* cur = smem + b * STAGE_BYTES;
-      if (s + 1 == nst) at_last();
       compute(cur);
       extra(cur);
       if (s + 1 < nst) {
-        if (s + 2 < nst)
-          wait_vmcnt<PPW>();
-        else
-          wait_vmcnt<0>();
+        if (s + 2 < nst) {
+          if (xl)
+            wait_vmcnt<PPW + XL>();
+          else
+            wait_vmcnt<PPW>();
+        } else {
+          if (xl)
+            wait_vmcnt<XL>();
+          else
+            wait_vmcnt<0>();
+        }
         step_barrier();
       }
       b = (b + 1 == NBUF) ? 0 : b + 1;
     }
+    return true;
   }
 
   // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
@@ -706,7 +743,8 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
                                                        double* __restrict__ H, double* __restrict__ SH,
                                                        int* __restrict__ stop_iter, int* __restrict__ stop_reason,
                                                        int* __restrict__ unchanged, int* __restrict__ classes,
-                                                       long cls_ld, int* __restrict__ n_stopped) {
+                                                       long cls_ld, int* __restrict__ n_stopped,
+                                                       double* __restrict__ SHP, int* __restrict__ colact) {
   __shared__ double sw[KMAX * KMAX];
   __shared__ double Hc[KMAX * HCH];
   __shared__ double Hn[KMAX * HCH];
@@ -801,7 +839,12 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
   if (tid < npairs) {
     SH[me.sq_off + pa * k + pb] = shacc;
     SH[me.sq_off + pb * k + pa] = shacc;
+    if (SHP) {   // the panel-row copy for the W update: row = global column c0 + a, KMAX doubles
+      SHP[(long)(c0 + pa) * KMAX + pb] = shacc;
+      SHP[(long)(c0 + pb) * KMAX + pa] = shacc;
+    }
   }
+  if (colact && tid < k) colact[c0 + tid] = iter;   // this restart's columns take part in the W update
   if (check && stop_rule == STOP_REF_COMPAT) {
     const int nwin = k < n ? k : n;
     if (tid < nwin) {
@@ -1133,6 +1176,105 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw2(int iter, const double*
       if (!c_act[c]) continue;
 #pragma unroll
       for (int nb = 0; nb < TT::NB; ++nb) {
+        const double v = VARIANT == 4 ? tl.acc[mb][nb][reg] : mu_rule(w0[mb][nb][reg], tl.acc[mb][nb][reg], e[nb][reg]);
+        if (VARIANT != 3 || v == (double)iter * 1.5e300) wdst[(long)c * m_pad + 16 * nb] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3 v4 "ahtw4": F = A h^T on the 3-stage GTile ring (one panel x 128 genes, 4 waves 1 x 4, 72 KiB)
+// + 8 KiB of h h^T rows = 80 KiB: two workgroups per CU.  Column state lives in registers: each wave
+// reads the panel's 64 ColInfo entries (lane = column), the active set is a 64-bit ballot of
+// colact[c] == iter (k_hupdate stamps its restart's columns with the iteration it ran) and the
+// E-operand rows' (lc0, k) come by lane shuffles.  These setup loads are issued after the first DMA
+// stages, so they overlap them.  The h h^T rows are read from SHP (panel-row layout
+// written by k_hupdate), one coalesced 8 KiB block.  W0 is loaded in the D layout right after the
+// last DMA issue (two stages before the end) and is the B operand of E = W0 (h h^T) directly.
+// ---------------------------------------------------------------------------------------------
+using TileW4 = GTile<64, 128, 1, 4, 3>;
+constexpr int AHTW4_SH = TileW4::LDS_BYTES;
+constexpr int AHTW4_LDS = AHTW4_SH + PANEL * KMAX * 8;
+static_assert(AHTW4_LDS <= 81920, "two workgroups per CU");
+
+template <int VARIANT>
+static __global__ __launch_bounds__(256, 2) void k_ahtw4(int iter, const double* __restrict__ H, long n_pad,
+                                                         const double* __restrict__ Arm, long m_pad,
+                                                         double* __restrict__ W, const double* __restrict__ SHP,
+                                                         const ColInfo* __restrict__ ci,
+                                                         const int* __restrict__ colact, int npanels, int ngt) {
+  __shared__ __attribute__((aligned(1024))) char smem[AHTW4_LDS];
+  double* SHl = reinterpret_cast<double*>(smem + AHTW4_SH);
+  int p, gt;
+  ahtw_map(xcd_item(blockIdx.x, npanels * ngt), npanels, ngt, p, gt);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  ColInfo cc;
+  uint64_t actmask = 0;
+  TileW4 tl;
+  tl.zero();
+  const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GT + 32 * w + (lane & 15);
+  double w0[TileW4::MB][TileW4::NB][4];
+  const bool live = tl.template run<TileW4::MB * TileW4::NB * 4>(
+      H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GT * n_pad, n_pad, 0, (int)n_pad, smem,
+      [&] {   // setup loads, independent of each other, overlapping the first stages' DMA
+        cc = ci[(long)p * PANEL + lane];
+        const int ca = colact[(long)p * PANEL + lane];
+        const d2* src = reinterpret_cast<const d2*>(SHP + (long)p * PANEL * KMAX);
+        d2 shv[PANEL * KMAX / 2 / 256];
+#pragma unroll
+        for (int j = 0; j < PANEL * KMAX / 2 / 256; ++j) shv[j] = src[tid + 256 * j];
+        actmask = __ballot(ca == iter);   // the column's restart ran k_hupdate at this iteration
+        if (actmask == 0) return false;   // idle panel (the same answer in every wave)
+#pragma unroll
+        for (int j = 0; j < PANEL * KMAX / 2 / 256; ++j) reinterpret_cast<d2*>(SHl)[tid + 256 * j] = shv[j];
+        return true;   // SHl is published by the ring prologue's barrier
+      },
+      [](const char*) {},
+      [&] {
+#pragma unroll
+        for (int mb = 0; mb < TileW4::MB; ++mb)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+            for (int nb = 0; nb < TileW4::NB; ++nb)
+              w0[mb][nb][reg] = (VARIANT == 1 || VARIANT == 4)
+                                    ? 1.0
+                                    : wsrc[(long)(16 * mb + (lane >> 4) + 4 * reg) * m_pad + 16 * nb];
+      });
+  if (!live) return;
+  double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GT + 32 * w + (lane & 15);
+#pragma unroll
+  for (int mb = 0; mb < TileW4::MB; ++mb) {
+    const int ra = 16 * mb + (lane & 15);
+    const int alc = __shfl(cc.lc0, ra);
+    const int ak = (VARIANT == 2 || VARIANT == 4 || !((actmask >> ra) & 1)) ? 0 : __shfl(cc.k, ra);
+    int lo = ak ? alc : PANEL, hi = ak ? alc + ak : 0;
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) {
+      lo = min(lo, __shfl_xor(lo, off));
+      hi = max(hi, __shfl_xor(hi, off));
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    d4 e[TileW4::NB];
+#pragma unroll
+    for (int nb = 0; nb < TileW4::NB; ++nb) e[nb] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (4 * q + 3 < lo || 4 * q >= hi) continue;   // wave-uniform
+      const int bb = 4 * q + (lane >> 4) - alc;
+      const double av = (bb >= 0 && bb < ak) ? SHl[ra * KMAX + bb] : 0.0;
+#pragma unroll
+      for (int nb = 0; nb < TileW4::NB; ++nb)
+        e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, w0[q >> 2][nb][q & 3], e[nb], 0, 0, 0);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int c = 16 * mb + (lane >> 4) + 4 * reg;
+      if (!((actmask >> c) & 1)) continue;
+#pragma unroll
+      for (int nb = 0; nb < TileW4::NB; ++nb) {
         const double v = VARIANT == 4 ? tl.acc[mb][nb][reg] : mu_rule(w0[mb][nb][reg], tl.acc[mb][nb][reg], e[nb][reg]);
         if (VARIANT != 3 || v == (double)iter * 1.5e300) wdst[(long)c * m_pad + 16 * nb] = v;
       }

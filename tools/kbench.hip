@@ -153,6 +153,16 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dci, ci.data(), sizeof(ColInfo) * ci.size(), hipMemcpyHostToDevice));
   }
   CK(hipMalloc(&SH, sizeof(double) * sw_total));
+  double* SHP;
+  CK(hipMalloc(&SHP, sizeof(double) * cols * KMAX));
+  int* colact;
+  CK(hipMalloc(&colact, sizeof(int) * cols));
+  {
+    std::vector<int> ca(cols, 0);
+    for (const RestartInfo& r : ri)
+      for (int a = 0; a < r.k; ++a) ca[r.col0 + a] = 1;   // iteration 1
+    CK(hipMemcpy(colact, ca.data(), sizeof(int) * cols, hipMemcpyHostToDevice));
+  }
   CK(hipMalloc(&dri, sizeof(RestartInfo) * nact));
   CK(hipMalloc(&dprb, sizeof(int) * npanels));
   CK(hipMalloc(&dpre, sizeof(int) * npanels));
@@ -170,6 +180,11 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(Arm, h.data(), sizeof(double) * m_pad * n_pad, hipMemcpyHostToDevice));
     std::vector<double> s(sw_total, 1e-3);
     CK(hipMemcpy(SH, s.data(), sizeof(double) * sw_total, hipMemcpyHostToDevice));
+    std::vector<double> sp((size_t)cols * KMAX, 0.0);
+    for (const RestartInfo& r : ri)
+      for (int a = 0; a < r.k; ++a)
+        for (int b = 0; b < r.k; ++b) sp[(size_t)(r.col0 + a) * KMAX + b] = 1e-3;
+    CK(hipMemcpy(SHP, sp.data(), sizeof(double) * sp.size(), hipMemcpyHostToDevice));
   }
   CK(hipMemcpy(dri, ri.data(), sizeof(RestartInfo) * nact, hipMemcpyHostToDevice));
   CK(hipMemcpy(dprb, prb.data(), sizeof(int) * npanels, hipMemcpyHostToDevice));
@@ -252,8 +267,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(W2, h.data(), wn * 8, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_ahtw, dim3(npanels * ngt), dim3(NT), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SH, dprb, dpre, dri,
                        dci, stop, npanels, ngt);
-    hipLaunchKernelGGL((k_ahtw2<0, 1>), dim3(npanels * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm, m_pad, W2, SH, dprb, dpre, dri,
-                       dci, stop, npanels, ngt);
+    hipLaunchKernelGGL(k_ahtw4<0>, dim3(npanels * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm, m_pad, W2, SHP, dci, colact,
+                       npanels, ngt);
     CK(hipDeviceSynchronize());
     std::vector<double> a1(wn), a2(wn);
     CK(hipMemcpy(a1.data(), W, wn * 8, hipMemcpyDeviceToHost));
@@ -266,7 +281,7 @@ int main(int argc, char** argv) {
       mx = std::max(mx, std::fabs(a1[i]));
       nbad += d > 1e-12 * std::fabs(a1[i]);
     }
-    printf("ahtw2 vs ahtw: W max rel diff %.3e (max %.3e), %zu entries off by >1e-12\n", md, mx, nbad);
+    printf("ahtw4 vs ahtw: W max rel diff %.3e (max %.3e), %zu entries off by >1e-12\n", md, mx, nbad);
     CK(hipFree(W2));
 #define AHTW2_VAR(V, label)                                                                                  \
     t = timeit([&] {                                                                                        \
@@ -291,6 +306,17 @@ int main(int argc, char** argv) {
     AHTW3_VAR(1, "no W0 load")
     AHTW3_VAR(2, "no E")
     AHTW3_VAR(4, "main only")
+#define AHTW4_VAR(V, label)                                                                                  \
+    t = timeit([&] {                                                                                        \
+      hipLaunchKernelGGL(k_ahtw4<V>, dim3(npanels * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SHP, dci, colact, \
+                         npanels, ngt);                                                                     \
+    }, reps);                                                                                               \
+    printf("k_ahtw4 %-14s %8.3f ms  %6.1f TF useful\n", label, t, useful / t / 1e9);
+    AHTW4_VAR(0, "")
+    AHTW4_VAR(0, "")
+    AHTW4_VAR(1, "no W0 load")
+    AHTW4_VAR(2, "no E")
+    AHTW4_VAR(4, "main only")
   }
 #define AHTW_VAR(V, label)                                                                                  \
   t = timeit([&] {                                                                                          \
@@ -303,7 +329,7 @@ int main(int argc, char** argv) {
   AHTW_VAR(3, "no W store")
   t = timeit([&] {
     hipLaunchKernelGGL(k_hupdate, dim3(nact), dim3(NT), 0, 0, 1, 10000, 0, dri, n, n_pad, Gpart, g_ld, g_split, nsplit,
-                       SWpart, sw_total, Hh, SH, stop, reason, unch, cls, 512L, nst);
+                       SWpart, sw_total, Hh, SH, stop, reason, unch, cls, 512L, nst, SHP, colact);
   }, reps);
   printf("k_hupdate    %8.3f ms\n", t);
   return 0;
