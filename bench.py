@@ -218,10 +218,11 @@ def main():
         if os.path.exists(tp) and args.config == "C3":
             try:
                 pm = json.load(open(tp))
-                key = "k_wta" if dom == "wta" else ("k_ahtw_t" if "k_ahtw_t" in pm else "k_ahtw")
+                key = "k_wta2" if dom == "wta" else "k_ahtw4"
                 if key in pm:
                     roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
-                    roof["traffic_unit"] = "bytes per full-load launch (rocprofv3 PMC, profiles/pmc_traffic.json)"
+                    roof["traffic_unit"] = ("HBM bytes per launch, averaged over every launch of one C3 sweep like "
+                                            "`achieved` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_traffic.json)")
             except Exception as ex:
                 log(f"[bench] could not read {tp}: {ex!r}")
 

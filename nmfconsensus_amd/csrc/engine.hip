@@ -112,8 +112,10 @@ std::vector<uint32_t> make_jump_table(int nchunks) {
 
 enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID_N = 5 };
 
-// Packing of a restart list into 64-column panels (sequential fill, k-descending order given);
-// panel count rounded up to a multiple of WTA_NPT (the large W^T A tile spans that many panels).
+// Packing of a restart list into 64-column panels by first-fit decreasing (k descending, ties by rid;
+// a restart never straddles a panel), so the k = 10 / 6 / 5 panels' spare columns take small-k
+// restarts; panel count rounded up to a multiple of WTA_NPT (the large W^T A tile spans that many
+// panels).  Placement never changes a result bit (DESIGN.md "Determinism").
 constexpr int WTA_NPT = 4;
 struct Packing {
   std::vector<RestartInfo> ri;   // active list, panel-contiguous
@@ -124,21 +126,31 @@ struct Packing {
 
 Packing pack(const std::vector<RestartInfo>& in) {
   Packing pk;
-  int fill = PANEL, np = -1;
-  for (size_t q = 0; q < in.size(); ++q) {
-    RestartInfo r = in[q];
-    if (fill + r.k > PANEL) {
-      ++np;
-      fill = 0;
-      pk.prb.push_back((int)q);
-      pk.pre.push_back((int)q);
+  std::vector<RestartInfo> srt(in);
+  std::stable_sort(srt.begin(), srt.end(), [](const RestartInfo& a, const RestartInfo& b) {
+    return a.k != b.k ? a.k > b.k : a.rid < b.rid;
+  });
+  std::vector<int> fill;                          // per panel: columns used
+  std::vector<std::vector<RestartInfo>> members;  // per panel, in column order
+  int first_open = 0;                             // panels before it have < KMIN free columns
+  for (RestartInfo r : srt) {
+    int p = first_open;
+    while (p < (int)fill.size() && fill[p] + r.k > PANEL) ++p;
+    if (p == (int)fill.size()) {
+      fill.push_back(0);
+      members.emplace_back();
     }
-    r.col0 = np * PANEL + fill;
-    fill += r.k;
-    pk.ri.push_back(r);
-    pk.pre[np] = (int)q + 1;
+    r.col0 = p * PANEL + fill[p];
+    fill[p] += r.k;
+    members[p].push_back(r);
+    while (first_open < (int)fill.size() && fill[first_open] > PANEL - 2) ++first_open;   // k >= 2
   }
-  pk.npanels = np + 1;
+  for (size_t p = 0; p < members.size(); ++p) {
+    pk.prb.push_back((int)pk.ri.size());
+    for (const RestartInfo& r : members[p]) pk.ri.push_back(r);
+    pk.pre.push_back((int)pk.ri.size());
+  }
+  pk.npanels = (int)members.size();
   if (pk.npanels == 0) {
     pk.npanels = 1;
     pk.prb = {0};
@@ -622,8 +634,10 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       for (const RestartInfo& r : pk.ri) (si[r.rid] ? gone : live).push_back(r);
       if (archive(gone)) return -1;
       Packing np = pack(live);
+      std::vector<int> old_col(nj, -1);
+      for (const RestartInfo& r : live) old_col[r.rid] = r.col0;
       std::vector<MoveJob> mv(np.ri.size());
-      for (size_t x = 0; x < np.ri.size(); ++x) mv[x] = {live[x].col0, np.ri[x].col0, np.ri[x].k};
+      for (size_t x = 0; x < np.ri.size(); ++x) mv[x] = {old_col[np.ri[x].rid], np.ri[x].col0, np.ri[x].k};
       if (!mv.empty()) {
         HCHECK(hipMemcpyAsync(e->moves.p, mv.data(), sizeof(MoveJob) * mv.size(), hipMemcpyHostToDevice, st));
         {

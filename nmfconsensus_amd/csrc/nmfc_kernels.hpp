@@ -736,25 +736,34 @@ static __global__ __launch_bounds__(WR * WC * 64) void k_wta2(const double* __re
 //   work1 = W0^T W0 = sum of the per-chunk Gram partials (nmf_mu.c:176); work2 = work1 H0 (:178);
 //   H <- mu_rule(H, G, work2) (:184-191); SH = H H^T (:200); stability check (:253-282).
 // ---------------------------------------------------------------------------------------------
-static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, int stop_rule,
-                                                       const RestartInfo* __restrict__ ri, int n, long n_pad,
-                                                       const double* __restrict__ Gpart, long g_ld, long g_split,
-                                                       int nsplit, const double* __restrict__ SWpart, long sw_total,
-                                                       double* __restrict__ H, double* __restrict__ SH,
-                                                       int* __restrict__ stop_iter, int* __restrict__ stop_reason,
-                                                       int* __restrict__ unchanged, int* __restrict__ classes,
-                                                       long cls_ld, int* __restrict__ n_stopped,
-                                                       double* __restrict__ SHP, int* __restrict__ colact) {
-  __shared__ double sw[KMAX * KMAX];
-  __shared__ double Hc[KMAX * HCH];
-  __shared__ double Hn[KMAX * HCH];
-  __shared__ double win[KMAX * KMAX];
-  __shared__ int changed;
-  const RestartInfo me = ri[blockIdx.x];
+struct HupdSmem {
+  double sw[KMAX * KMAX];
+  double Hn[KMAX * HCH];
+  double win[KMAX * KMAX];
+  double shp[NT];
+  int changed;
+};
+
+// The body for rank K (compile time): every per-sample loop over the k factors is unrolled, so the
+// k loads of one chunk round are issued together and consumed after.
+template <int K>
+__device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int maxiter, int stop_rule, int n,
+                                             long n_pad, const double* __restrict__ Gpart, long g_ld, long g_split,
+                                             int nsplit, const double* __restrict__ SWpart, long sw_total,
+                                             double* __restrict__ H, double* __restrict__ SH,
+                                             int* __restrict__ stop_iter, int* __restrict__ stop_reason,
+                                             int* __restrict__ unchanged, int* __restrict__ classes, long cls_ld,
+                                             int* __restrict__ n_stopped, double* __restrict__ SHP,
+                                             int* __restrict__ colact, HupdSmem& sm) {
+  double* sw = sm.sw;
+  double* Hn = sm.Hn;
+  double* win = sm.win;
+  double* shp = sm.shp;
+  int& changed = sm.changed;
   const int rid = me.rid;
-  if (stop_iter[rid] != 0) return;
   const int tid = threadIdx.x;
-  const int c0 = me.col0, k = me.k;
+  constexpr int k = K;
+  const int c0 = me.col0;
   const bool check = (stop_rule != STOP_FIXED) && iter > 1 && (iter % 2 == 0);
   if (tid == 0) changed = 0;
   for (int idx = tid; idx < k * k; idx += NT) {
@@ -771,10 +780,14 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
     sw[(idx / k) * KMAX + (idx % k)] = sacc;
   }
   for (int idx = tid; idx < KMAX * KMAX; idx += NT) win[idx] = 0.0;
+  // h h^T: T threads per (pa, pb) pair (T a function of k only); thread pq of a pair sums the samples
+  // j = pq (mod T) in order, and the T partials are added in pq order at the end.
   const int npairs = k * (k + 1) / 2;
+  const int T = (npairs * 8 <= NT) ? 8 : (npairs * 4 <= NT) ? 4 : (npairs * 2 <= NT) ? 2 : 1;
+  const int pid = tid / T, pq = tid % T;
   int pa = 0, pb = 0;
-  if (tid < npairs) {
-    int t = tid;
+  if (pid < npairs) {
+    int t = pid;
     while (t >= k - pa) {
       t -= k - pa;
       ++pa;
@@ -787,25 +800,45 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
   for (int j0 = 0; j0 < n; j0 += HCH) {
     const int j = j0 + tid;
     const bool valid = j < n;
-    for (int a = 0; a < k; ++a) Hc[a * HCH + tid] = valid ? H[(long)(c0 + a) * n_pad + j] : 0.0;
+    // this sample's k entries of H and of the chunk-summed W^T A (partials added in chunk order);
+    // the k loads of one chunk round are independent, so they are in flight together
+    double hc[K], gs[K];
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+      hc[a] = valid ? H[(long)(c0 + a) * n_pad + j] : 0.0;
+      gs[a] = 0.0;
+    }
+    if (valid) {
+      const double* gsrc = Gpart + (long)c0 * g_ld + j;
+      int sp = 0;
+      for (; sp + 1 < nsplit; sp += 2) {   // two chunk rounds: 2K independent loads, then the adds
+        double v0[K], v1[K];
+#pragma unroll
+        for (int a = 0; a < K; ++a) {
+          v0[a] = gsrc[(long)sp * g_split + (long)a * g_ld];
+          v1[a] = gsrc[(long)(sp + 1) * g_split + (long)a * g_ld];
+        }
+#pragma unroll
+        for (int a = 0; a < K; ++a) gs[a] = ((sp == 0) ? v0[a] : gs[a] + v0[a]) + v1[a];
+      }
+      if (sp < nsplit) {
+        double v0[K];
+#pragma unroll
+        for (int a = 0; a < K; ++a) v0[a] = gsrc[(long)sp * g_split + (long)a * g_ld];
+#pragma unroll
+        for (int a = 0; a < K; ++a) gs[a] = (sp == 0) ? v0[a] : gs[a] + v0[a];
+      }
+    }
     int best = 0;
-    for (int a = 0; a < k; ++a) {
+    double bestv = 0.0;
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
       double hn = 0.0;
       if (valid) {
-        const long goff = (long)(c0 + a) * g_ld + j;
-        // chunk partials summed in chunk order; loads issued 8 at a time for memory-level parallelism
-        double gsum = 0.0;
-        for (int sp0 = 0; sp0 < nsplit; sp0 += 8) {
-          double v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = (sp0 + u < nsplit) ? Gpart[(long)(sp0 + u) * g_split + goff] : 0.0;
-#pragma unroll
-          for (int u = 0; u < 8; ++u)
-            if (sp0 + u < nsplit) gsum = (sp0 + u == 0) ? v[u] : gsum + v[u];
-        }
         double d = 0.0;
-        for (int bb = 0; bb < k; ++bb) d = fma(sw[a * KMAX + bb], Hc[bb * HCH + tid], d);
-        hn = mu_rule(Hc[a * HCH + tid], gsum, d);
+#pragma unroll
+        for (int bb = 0; bb < K; ++bb) d = fma(sw[a * KMAX + bb], hc[bb], d);
+        hn = mu_rule(hc[a], gs[a], d);
         H[(long)(c0 + a) * n_pad + j] = hn;
         if (stop_rule == STOP_REF_COMPAT) {
           // flat column-major index of (a, j) in the k x n buffer; window i reads [i*n, i*n + k)
@@ -818,7 +851,10 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
         }
       }
       Hn[a * HCH + tid] = hn;
-      if (a > 0 && hn > Hn[best * HCH + tid]) best = a;
+      if (a == 0 || hn > bestv) {   // first maximum
+        best = a;
+        bestv = hn;
+      }
     }
     if (check && stop_rule == STOP_ARGMAX_STABLE && valid) {
       int* cl = classes + (long)rid * cls_ld + j;
@@ -828,20 +864,24 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
       }
     }
     __syncthreads();
-    if (tid < npairs) {
+    if (pid < npairs) {
       const int cnt = min(HCH, n - j0);
       const double* ha = Hn + pa * HCH;
       const double* hb = Hn + pb * HCH;
-      for (int q = 0; q < cnt; ++q) shacc = fma(ha[q], hb[q], shacc);
+      for (int q = pq; q < cnt; q += T) shacc = fma(ha[q], hb[q], shacc);
     }
     __syncthreads();
   }
-  if (tid < npairs) {
-    SH[me.sq_off + pa * k + pb] = shacc;
-    SH[me.sq_off + pb * k + pa] = shacc;
+  shp[tid] = shacc;
+  __syncthreads();
+  if (pid < npairs && pq == 0) {
+    double s = shp[tid];
+    for (int q = 1; q < T; ++q) s += shp[tid + q];
+    SH[me.sq_off + pa * k + pb] = s;
+    SH[me.sq_off + pb * k + pa] = s;
     if (SHP) {   // the panel-row copy for the W update: row = global column c0 + a, KMAX doubles
-      SHP[(long)(c0 + pa) * KMAX + pb] = shacc;
-      SHP[(long)(c0 + pb) * KMAX + pa] = shacc;
+      SHP[(long)(c0 + pa) * KMAX + pb] = s;
+      SHP[(long)(c0 + pb) * KMAX + pa] = s;
     }
   }
   if (colact && tid < k) colact[c0 + tid] = iter;   // this restart's columns take part in the W update
@@ -877,6 +917,32 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
       atomicAdd(n_stopped, 1);
     }
   }
+}
+
+static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, int stop_rule,
+                                                       const RestartInfo* __restrict__ ri, int n, long n_pad,
+                                                       const double* __restrict__ Gpart, long g_ld, long g_split,
+                                                       int nsplit, const double* __restrict__ SWpart, long sw_total,
+                                                       double* __restrict__ H, double* __restrict__ SH,
+                                                       int* __restrict__ stop_iter, int* __restrict__ stop_reason,
+                                                       int* __restrict__ unchanged, int* __restrict__ classes,
+                                                       long cls_ld, int* __restrict__ n_stopped,
+                                                       double* __restrict__ SHP, int* __restrict__ colact) {
+  __shared__ HupdSmem sm;
+  const RestartInfo me = ri[blockIdx.x];
+  if (stop_iter[me.rid] != 0) return;
+#define NMFC_HUPD_CASE(KK)                                                                                      \
+  case KK:                                                                                                     \
+    hupdate_body<KK>(me, iter, maxiter, stop_rule, n, n_pad, Gpart, g_ld, g_split, nsplit, SWpart, sw_total, H, SH, \
+                     stop_iter, stop_reason, unchanged, classes, cls_ld, n_stopped, SHP, colact, sm);          \
+    break;
+  switch (me.k) {
+    NMFC_HUPD_CASE(2) NMFC_HUPD_CASE(3) NMFC_HUPD_CASE(4) NMFC_HUPD_CASE(5) NMFC_HUPD_CASE(6)
+    NMFC_HUPD_CASE(7) NMFC_HUPD_CASE(8) NMFC_HUPD_CASE(9) NMFC_HUPD_CASE(10) NMFC_HUPD_CASE(11)
+    NMFC_HUPD_CASE(12) NMFC_HUPD_CASE(13) NMFC_HUPD_CASE(14) NMFC_HUPD_CASE(15) NMFC_HUPD_CASE(16)
+    default: break;
+  }
+#undef NMFC_HUPD_CASE
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -2,8 +2,11 @@
 
 Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE are
 in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so it is
-doubled; WRITE_SIZE is taken as is.  Only full-load launches are averaged (the first 100 launches of
-each kernel: every restart is still running before iteration 400).  Prints JSON."""
+doubled; WRITE_SIZE is taken as is.
+
+Two averages per kernel: over ALL launches of the profiled sweep (what bench.py's roofline `achieved`
+is averaged over: every launch of one REF_COMPAT sweep) and over the full-load launches (the first
+100: every restart is still running before iteration 400).  Prints JSON."""
 import collections
 import csv
 import glob
@@ -21,12 +24,16 @@ for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             kn = row["Kernel_Name"].split("(")[0].split("::")[-1].split("<")[0]
             disp = int(row["Dispatch_Id"])
             per[kn][disp] = per[kn].get(disp, 0.0) + float(row["Counter_Value"])
+    scale = 2.0 if counter == "FETCH_SIZE" else 1.0
     for kn, d in per.items():
-        vals = [d[k] for k in sorted(d)][:100]
-        kib = sum(vals) / max(len(vals), 1)
-        scale = 2.0 if counter == "FETCH_SIZE" else 1.0
-        out.setdefault(kn, {})[counter + "_bytes_per_launch"] = kib * 1024.0 * scale
-        out[kn]["launches_averaged"] = len(vals)
+        vals = [d[k] for k in sorted(d)]
+        full = vals[:100]
+        o = out.setdefault(kn, {})
+        o[counter + "_bytes_per_launch"] = sum(vals) / max(len(vals), 1) * 1024.0 * scale
+        o[counter + "_bytes_per_full_launch"] = sum(full) / max(len(full), 1) * 1024.0 * scale
+        o["launches"] = len(vals)
 for kn, d in out.items():
     d["hbm_bytes_per_launch"] = d.get("FETCH_SIZE_bytes_per_launch", 0.0) + d.get("WRITE_SIZE_bytes_per_launch", 0.0)
+    d["hbm_bytes_per_full_launch"] = (d.get("FETCH_SIZE_bytes_per_full_launch", 0.0) +
+                                      d.get("WRITE_SIZE_bytes_per_full_launch", 0.0))
 print(json.dumps(out, indent=1))
