@@ -176,6 +176,7 @@ struct nmfc_engine {
   long m_pad = 0, n_pad = 0, n_cols_pad = 0;
   int kchunk = 0, nsplit = 0, ngt = 0;
   int ncu = 256;   // compute units (grid-size heuristics only)
+  int force_wta = -1, force_ahtw = -1;   // tile-shape overrides (env NMFC_WTA_TILE / NMFC_AHTW_TILE)
   DevBuf Acm, Arm;
   // per-run buffers (grow-only)
   DevBuf W[2], H[2], Gpart, SWpart, SH, SHP, colact, Hfin, Wfin;
@@ -288,6 +289,14 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev) == hipSuccess && ncu > 0) e->ncu = ncu;
+  }
+  if (const char* s = getenv("NMFC_WTA_TILE")) {
+    const std::string v(s);
+    e->force_wta = v == "big" ? 0 : v == "small" ? 1 : v == "tiny" ? 2 : -1;
+  }
+  if (const char* s = getenv("NMFC_AHTW_TILE")) {
+    const std::string v(s);
+    e->force_ahtw = v == "128" ? 0 : v == "64" ? 1 : -1;
   }
   if ((err = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", err);
   if ((err = hipHostMalloc((void**)&e->h_stopped, 2 * sizeof(int), 0)) != hipSuccess) return fail("hipHostMalloc", err);
@@ -564,8 +573,18 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   for (;;) {
     if (it < opts.maxiter) {
       const int chunk = std::min(opts.check_every, opts.maxiter - it);
-      const bool wta_big = (long)e->nsplit * (pk.npanels / WTA_NPT) * ntj >= 2L * e->ncu;
-      const int grid_ahtw = pk.npanels * e->ngt;
+      // tile shapes by grid size (a speed choice only: every shape sums in the canonical K order)
+      bool wta_big = (long)e->nsplit * (pk.npanels / WTA_NPT) * ntj >= 2L * e->ncu;
+      bool wta_tiny = !wta_big && (long)e->nsplit * pk.npanels * 2 * ntj <= 2L * e->ncu;
+      // A h^T tiles: 1 panel x 128 genes, or 1 panel x 64 genes for small grids (twice the workgroups)
+      bool ahtw_small = (long)pk.npanels * e->ngt <= 8L * e->ncu;
+      if (e->force_wta >= 0) {   // NMFC_WTA_TILE (tests: every shape must give the same bits)
+        wta_big = e->force_wta == 0;
+        wta_tiny = e->force_wta == 2;
+      }
+      if (e->force_ahtw >= 0) ahtw_small = e->force_ahtw == 1;
+      const int ngt_ahtw = e->ngt * (ahtw_small ? 2 : 1);
+      const int grid_ahtw = pk.npanels * ngt_ahtw;
       for (int c = 1; c <= chunk; ++c) {
         const int iter = it + c;
         {
@@ -582,9 +601,15 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
                                e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
                                sw_total);
-          } else {
+          } else if (!wta_tiny) {
             hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1>), dim3(e->nsplit * pk.npanels * 2 * ntj), dim3(256), 0, st,
                                e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, pk.npanels, 2 * ntj, e->nsplit,
+                               e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
+                               e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
+                               e->SWpart.as<double>(), sw_total);
+          } else {   // few live panels: 1-panel x 32-sample tiles, two 16x16 blocks per wave (short chains)
+            hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1>), dim3(e->nsplit * pk.npanels * 4 * ntj), dim3(256), 0, st,
+                               e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, pk.npanels, 4 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
                                e->SWpart.as<double>(), sw_total);
@@ -601,9 +626,11 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         }
         {
           TimedLaunch tl(e, KID_AHTW);
-          hipLaunchKernelGGL(k_ahtw4<0>, dim3(grid_ahtw), dim3(256), 0, st, iter, e->H[cur].as<double>(), e->n_pad,
-                             e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(), e->SHP.as<double>(),
-                             e->colinfo.as<ColInfo>(), e->colact.as<int>(), pk.npanels, e->ngt);
+          auto ka = ahtw_small ? k_ahtw4<0, GT / 2> : k_ahtw4<0, GT>;
+          hipLaunchKernelGGL(ka, dim3(grid_ahtw), dim3(256), 0, st, iter,
+                             e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
+                             e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), pk.npanels,
+                             ngt_ahtw);
         }
       }
       HCHECK(hipGetLastError());

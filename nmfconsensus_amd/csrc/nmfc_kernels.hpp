@@ -1259,41 +1259,43 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw2(int iter, const double*
 // written by k_hupdate), one coalesced 8 KiB block.  W0 is loaded in the D layout right after the
 // last DMA issue (two stages before the end) and is the B operand of E = W0 (h h^T) directly.
 // ---------------------------------------------------------------------------------------------
-using TileW4 = GTile<64, 128, 1, 4, 3>;
-constexpr int AHTW4_SH = TileW4::LDS_BYTES;
-constexpr int AHTW4_LDS = AHTW4_SH + PANEL * KMAX * 8;
-static_assert(AHTW4_LDS <= 81920, "two workgroups per CU");
-
-template <int VARIANT>
+// GTG: genes per tile (128 at full load; 64 for small grids: half the MFMA chain per wave, twice the
+// workgroups).  ngt = m_pad / GTG.  Every shape accumulates in the canonical GTile K order.
+template <int VARIANT, int GTG = GT>
 static __global__ __launch_bounds__(256, 2) void k_ahtw4(int iter, const double* __restrict__ H, long n_pad,
                                                          const double* __restrict__ Arm, long m_pad,
                                                          double* __restrict__ W, const double* __restrict__ SHP,
                                                          const ColInfo* __restrict__ ci,
                                                          const int* __restrict__ colact, int npanels, int ngt) {
+  using TileW4 = GTile<64, GTG, 1, 4, 3>;
+  constexpr int AHTW4_SH = TileW4::LDS_BYTES;
+  constexpr int AHTW4_LDS = AHTW4_SH + PANEL * KMAX * 8;
+  static_assert(AHTW4_LDS <= 81920, "two workgroups per CU");
   __shared__ __attribute__((aligned(1024))) char smem[AHTW4_LDS];
   double* SHl = reinterpret_cast<double*>(smem + AHTW4_SH);
   int p, gt;
   ahtw_map(xcd_item(blockIdx.x, npanels * ngt), npanels, ngt, p, gt);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wc = tid >> 6;
   ColInfo cc;
   uint64_t actmask = 0;
   TileW4 tl;
   tl.zero();
-  const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GT + 32 * w + (lane & 15);
+  const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / 4) * wc + (lane & 15);
   double w0[TileW4::MB][TileW4::NB][4];
   const bool live = tl.template run<TileW4::MB * TileW4::NB * 4>(
-      H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GT * n_pad, n_pad, 0, (int)n_pad, smem,
+      H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
       [&] {   // setup loads, independent of each other, overlapping the first stages' DMA
         cc = ci[(long)p * PANEL + lane];
         const int ca = colact[(long)p * PANEL + lane];
         const d2* src = reinterpret_cast<const d2*>(SHP + (long)p * PANEL * KMAX);
-        d2 shv[PANEL * KMAX / 2 / 256];
+        constexpr int NSH = PANEL * KMAX / 2 / 256;
+        d2 shv[NSH];
 #pragma unroll
-        for (int j = 0; j < PANEL * KMAX / 2 / 256; ++j) shv[j] = src[tid + 256 * j];
+        for (int j = 0; j < NSH; ++j) shv[j] = src[tid + 256 * j];
         actmask = __ballot(ca == iter);   // the column's restart ran k_hupdate at this iteration
         if (actmask == 0) return false;   // idle panel (the same answer in every wave)
 #pragma unroll
-        for (int j = 0; j < PANEL * KMAX / 2 / 256; ++j) reinterpret_cast<d2*>(SHl)[tid + 256 * j] = shv[j];
+        for (int j = 0; j < NSH; ++j) reinterpret_cast<d2*>(SHl)[tid + 256 * j] = shv[j];
         return true;   // SHl is published by the ring prologue's barrier
       },
       [](const char*) {},
@@ -1309,7 +1311,7 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw4(int iter, const double*
                                     : wsrc[(long)(16 * mb + (lane >> 4) + 4 * reg) * m_pad + 16 * nb];
       });
   if (!live) return;
-  double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GT + 32 * w + (lane & 15);
+  double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / 4) * wc + (lane & 15);
 #pragma unroll
   for (int mb = 0; mb < TileW4::MB; ++mb) {
     const int ra = 16 * mb + (lane & 15);

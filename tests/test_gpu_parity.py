@@ -179,6 +179,33 @@ def test_ragged_shapes_vs_oracle(oracle, m, n, ks):
         assert np.all(r.H[j][:, 3] == 0.0)
 
 
+def test_tile_shapes_bit_identical(oracle):
+    # every W^T A / A h^T tile shape the engine picks by grid size sums in the same canonical K order:
+    # forcing each shape gives the same bits (so results never depend on how many restarts are live)
+    import os
+    from nmfconsensus_amd.nmf import Engine
+    rng = np.random.default_rng(11)
+    m, n, ks, T = 3001, 150, [2, 7, 10, 16], 12
+    A = np.asfortranarray(rng.random((m, n)) * 3.0)
+    runs = {}
+    try:
+        for wta in ("big", "small", "tiny"):
+            for ahtw in ("128", "64"):
+                os.environ["NMFC_WTA_TILE"], os.environ["NMFC_AHTW_TILE"] = wta, ahtw
+                with Engine(A) as eng:
+                    runs[(wta, ahtw)] = eng.run(ks, 3, maxiter=T, seed=5, stop_rule=0, want_factors=True)
+    finally:
+        os.environ.pop("NMFC_WTA_TILE", None)
+        os.environ.pop("NMFC_AHTW_TILE", None)
+    ref = runs[("big", "128")]
+    for key, r in runs.items():
+        for j in range(len(ks) * 3):
+            assert np.array_equal(r.W[j], ref.W[j]) and np.array_equal(r.H[j], ref.H[j]), (key, j)
+    W0, H0 = oracle.init_restart(5 + 3, m, n, 16)
+    Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, T, 0)
+    assert relfro(ref.W[3], Wo) < TOL and relfro(ref.H[3], Ho) < TOL
+
+
 def test_full_size_c3_shape_vs_oracle(oracle):
     # BASELINE config C3 shape (20000 x 500), k = 10, a few fixed iterations against the oracle
     from nmfconsensus_amd.nmf import Engine
