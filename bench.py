@@ -45,7 +45,14 @@ def _cpu_worker(args):
 
     A = planted_matrix(m, n)
     out = {}
-    if kind == "reference":
+    if kind == "brunet":
+        O = pyoracle.Oracle()
+        for k in ks:
+            W0, H0 = O.brunet_init(123 + k, m, n, k)
+            t0 = time.perf_counter()
+            O.brunet(A, W0, H0, T, 10 ** 6, 10)
+            out[k] = (time.perf_counter() - t0) / T
+    elif kind == "reference":
         lib = pyoracle.RefLib()
         for k in ks:
             W0, H0 = lib.generate_ran(123 + k, m, n, k)
@@ -62,10 +69,13 @@ def _cpu_worker(args):
     return out
 
 
-def cpu_baseline(m, n, ks, mean_iters_per_k, cores, T):
+def cpu_baseline(m, n, ks, mean_iters_per_k, cores, T, brunet=False):
     import multiprocessing as mp
 
-    kind = "reference" if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libnmf_ref.so")) else "port"
+    if brunet:
+        kind = "brunet"
+    else:
+        kind = "reference" if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libnmf_ref.so")) else "port"
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
     devnull = os.open(os.devnull, os.O_WRONLY)
@@ -83,12 +93,14 @@ def cpu_baseline(m, n, ks, mean_iters_per_k, cores, T):
     # sweep of R restarts per k on `cores` processes: CPU-seconds = R * sum_k t_iter(k) * I(k)
     per_restart_set = sum(t_iter[k] * mean_iters_per_k[k] for k in ks)
     value = len(ks) * cores / per_restart_set
+    what = {"reference": "reference libnmf nmf_mu (oracle/_ref, scipy OpenBLAS, 1 thread/process)",
+            "port": "oracle C restatement of nmf_mu", "brunet": "oracle C restatement of NMF.div (brunet_oracle.c)"}[kind]
     return {
         "value": value,
         "unit": "restarts/s",
         "cores": cores,
-        "kind": kind,
-        "sample": (f"{'reference libnmf nmf_mu (oracle/_ref, scipy OpenBLAS, 1 thread/process)' if kind == 'reference' else 'oracle C restatement'}"
+        "kind": "port" if kind == "brunet" else kind,
+        "sample": (f"{what}"
                    f" x {cores} concurrent processes, {T} iterations per k={ks[0]}..{ks[-1]} on the {m}x{n} matrix; "
                    f"restarts/s extrapolated with the GPU run's mean iterations per k; sample wall {wall:.1f} s"),
         "sec_per_iter": {str(k): t_iter[k] for k in ks},
@@ -100,7 +112,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4"])
+    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--maxiter", type=int, default=10000)
     ap.add_argument("--stop-rule", default="ref_compat", choices=["fixed", "ref_compat", "argmax_stable"])
     ap.add_argument("--restarts", type=int, default=None, help="override R (restarts per k)")
@@ -126,6 +138,9 @@ def main():
     from nmfconsensus_amd.nmf import Engine, cophenetic
     from nmfconsensus_amd.distributed import shard_range
     from nmfconsensus_amd import _lib
+
+    if args.config == "C5":
+        return bench_brunet(args, rank, world, local, dev)
 
     m, n, ks, R, desc = CONFIGS[args.config]
     if args.restarts:
@@ -252,6 +267,122 @@ def main():
                        "cophenetic_rho": {str(k): v for k, v in rho.items()}},
             "roofline": roof,
             "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def bench_brunet(args, rank, world, local, dev):
+    """BASELINE configs[4]: Brunet KL-divergence MU sweep (nmfc_brunet_*).  A step = the whole
+    nmfconsensus sweep (k = 2..10, R restarts each, NMF.div stop rule stopconv 40 / stopfreq 10,
+    maxniter 2000) with labels, int32 counts (RCCL all-reduce when N > 1), consensus and cophenetic.
+    Restarts are sharded over ranks (every rank runs its restart range for every k)."""
+    import numpy as np
+    import torch
+
+    from nmfconsensus_amd.synthetic import CONFIGS, planted_matrix
+    from nmfconsensus_amd.nmf import cophenetic
+    from nmfconsensus_amd.brunet import BrunetEngine
+    from nmfconsensus_amd.distributed import shard_range
+    from nmfconsensus_amd import _lib
+
+    m, n, ks, R, desc = CONFIGS["C5"]
+    if args.restarts:
+        R = args.restarts
+    nk = len(ks)
+    maxiter = min(args.maxiter, 2000)
+    A_host = planted_matrix(m, n)
+    A_dev = torch.from_numpy(A_host.T.copy()).to(dev)
+    torch.cuda.synchronize()
+    eng = BrunetEngine(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local)
+    counts = torch.zeros((nk, n, n), dtype=torch.int32, device=dev)
+    rb, re = shard_range(R, rank, world)
+    timing = not args.no_timing
+
+    def step():
+        res = eng.run(ks, R, maxiter=maxiter, seed=123456789, restart_begin=rb, restart_end=re,
+                      counts_device_ptr=counts.data_ptr())
+        if world > 1:
+            torch.distributed.all_reduce(counts, op=torch.distributed.ReduceOp.SUM)
+        cons = counts.to(torch.float64) / R
+        rho = {}
+        if rank == 0:
+            C = cons.cpu().numpy()
+            for i, k in enumerate(ks):
+                rho[k] = cophenetic(C[i])[0]
+        return res, rho
+
+    eng.set_timing(False)
+    for _ in range(args.warmup):
+        step()
+    eng.set_timing(timing)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    acc = {kid: [0, 0.0, 0.0] for kid in (_lib.BK_HNUM, _lib.BK_HUPD, _lib.BK_WUPD)}
+    iters_all, last = [], None
+    for _ in range(args.steps):
+        res, rho = step()
+        last = (res, rho)
+        iters_all.append(res.iters.copy())
+        for kid, a in acc.items():
+            c, ms, fl = eng.kernel_time(kid)
+            a[0] += c
+            a[1] += ms
+            a[2] += fl * c
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    res, rho = last
+    value = nk * R * args.steps / elapsed
+    its = np.concatenate(iters_all)
+    B = re - rb
+    mean_iter_k = {k: float(np.mean(res.iters[i * B:(i + 1) * B])) for i, k in enumerate(ks)}
+    log(f"[bench C5] rank {rank}: {nk * B} restarts/step, mean iters {its.mean():.1f} (max {its.max()}), "
+        f"step {elapsed / args.steps:.3f} s, engine {res.seconds_total:.3f} s")
+    roof = None
+    if timing and acc[_lib.BK_HNUM][0]:
+        kernels = {}
+        for name, kid in (("hnum", _lib.BK_HNUM), ("hupd", _lib.BK_HUPD), ("wupd", _lib.BK_WUPD)):
+            c, ms, fl = acc[kid]
+            kernels[name] = {"launches": c, "avg_ms": ms / max(c, 1)}
+            if fl:
+                kernels[name]["algo_flop_per_launch"] = fl / c
+                kernels[name]["tflops"] = fl / c / (ms / c * 1e-3) / 1e12
+        dom = max(("hnum", "wupd"), key=lambda s: kernels[s]["avg_ms"] * kernels[s]["launches"])
+        ach = kernels[dom]["tflops"]
+        roof = {"bound": "valu", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None, "kernels": kernels,
+                "note": "fp64 VALU (FMA + IEEE divide); peak = the 78.6 TF fp64 vector spec; flops count only the "
+                        "rank-k products (4 m n k per restart and kernel), not the m n divides"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        try:
+            cpu = cpu_baseline(m, n, ks, mean_iter_k, cores, max(2, args.cpu_iters // 20), brunet=True)
+        except Exception as ex:
+            log(f"[bench] cpu baseline failed: {ex!r}")
+    if rank == 0:
+        out = {
+            "metric": "NMF restarts/sec (Brunet KL-divergence MU, k=2..10 sweep, 20k×500 fp64) + fp64 roofline %",
+            "value": value, "unit": "restarts/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (planted 4-group matrix, splitmix64 seed 20261015; per-restart set.seed(rseed+i) runif init)",
+            "config": {"workload": f"C5: {desc}, NMF.div stopconv 40 stopfreq 10, maxniter {maxiter}", "m": m, "n": n,
+                       "ks": ks, "restarts_per_k": R, "jobs": nk * R,
+                       "parallelism": f"restarts sharded over {world} GPU(s), RCCL int32 all-reduce of counts",
+                       "mean_iterations": float(its.mean()), "max_iterations": int(its.max()),
+                       "cophenetic_rho": {str(k): v for k, v in rho.items()}},
+            "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     eng.close()

@@ -98,6 +98,39 @@ double nmfc_cophenetic(const double* C, int n, int32_t* order_out, int32_t* merg
 /* cutree(HC, k) membership (nmf.r:177) from a merge matrix produced by nmfc_cophenetic. 1-based. */
 int nmfc_cutree(const int32_t* merge, int n, int k, int32_t* membership_out);
 
+/* ---------------------------------------------------------------------------------------------
+ * Brunet KL-divergence MU restarts (BASELINE.json configs[4]).  The per-restart
+ * algorithm is the BROAD nmfconsensus script's NMF.div (Brunet et al. 2004), which the reference only
+ * names (commented-out call, test_nmf.r:29); restated in oracle/brunet_oracle.c, parity vs the
+ * reference unpinned.  Job order follows nmfconsensus: for k in ks, for restart i in 1..R, with
+ * set.seed(seed + i) then W <- runif(m*k), H <- runif(k*n) (R's Mersenne-Twister, bit-exact).
+ * Per-job output arrays are indexed (k index) * (restart_end - restart_begin) + (i - 1 - restart_begin);
+ * W/H outputs are job-major in that order (W m x k, H k x n, column-major).  counts/consensus as for
+ * nmfc_engine_run (membership = order(H[,j], decreasing=TRUE)[1], i.e. the first row of the maximum).
+ * --------------------------------------------------------------------------------------------- */
+typedef struct nmfc_brunet_opts {
+  int maxiter;        /* NMF.div maxniter (default 2000) */
+  int stopconv;       /* consecutive unchanged membership checks that stop a restart (default 40) */
+  int stopfreq;       /* iterations between membership checks (default 10) */
+  uint32_t seed;      /* nmfconsensus rseed: restart i (1-based) uses set.seed(seed + i) (default 123456789) */
+  int restart_begin;  /* shard [restart_begin, restart_end) of the restarts 0..R-1, for every k; end < 0 => R */
+  int restart_end;
+  int verbose;
+} nmfc_brunet_opts;
+
+typedef struct nmfc_brunet nmfc_brunet;
+
+void nmfc_brunet_default_opts(nmfc_brunet_opts* o);
+nmfc_brunet* nmfc_brunet_create(int device, const double* A, int m, int n, int a_on_device);
+void nmfc_brunet_destroy(nmfc_brunet* e);
+/* W_init/H_init (optional, host): every job of the shard in output order. Returns 0 or -1 (nmfc_last_error). */
+int nmfc_brunet_run(nmfc_brunet* e, const int* ks, int nk, int R, const nmfc_brunet_opts* opts, const double* W_init,
+                    const double* H_init, nmfc_result* out);
+void nmfc_brunet_set_timing(nmfc_brunet* e, int enable);
+/* kernel ids 0 = H-side quotient product (k_br_hnum), 1 = H update + check (k_br_hupd), 2 = W side
+ * (k_br_wupd); returns launches, fills accumulated event ms and algorithmic flop per launch. */
+long long nmfc_brunet_kernel_time(nmfc_brunet* e, int kernel_id, double* ms_out, double* flops_per_launch);
+
 /* Diagnostics. */
 const char* nmfc_last_error(void);
 const char* nmfc_version(void);

@@ -33,6 +33,14 @@ class Result(ctypes.Structure):
                 ("restart_iterations", ctypes.c_longlong), ("max_iter_run", c_int)]
 
 
+class BrunetOpts(ctypes.Structure):
+    _fields_ = [("maxiter", c_int), ("stopconv", c_int), ("stopfreq", c_int), ("seed", ctypes.c_uint32),
+                ("restart_begin", c_int), ("restart_end", c_int), ("verbose", c_int)]
+
+
+BK_HNUM, BK_HUPD, BK_WUPD = 0, 1, 2
+
+
 class OptionsT(ctypes.Structure):
     """options_t (libnmf/include/common.h:92-105)."""
     _fields_ = [("rep", c_int), ("init", c_int), ("min_init", c_int), ("max_init", c_int),
@@ -49,6 +57,8 @@ EXPORTED = [
     "nmfc_engine_create", "nmfc_engine_destroy", "nmfc_default_opts", "nmfc_engine_run", "nmfc_sweep",
     "nmfc_consensus", "nmfc_cophenetic", "nmfc_cutree", "nmfc_last_error", "nmfc_version", "nmfc_engine_kernel_time",
     "nmfc_engine_set_timing", "nmfc_engine_kernel_flops",
+    "nmfc_brunet_default_opts", "nmfc_brunet_create", "nmfc_brunet_destroy", "nmfc_brunet_run",
+    "nmfc_brunet_set_timing", "nmfc_brunet_kernel_time",
 ]
 
 _LIB = None
@@ -113,6 +123,19 @@ def lib() -> ctypes.CDLL:
     L.nmfc_engine_set_timing.restype = None
     L.nmfc_engine_kernel_flops.argtypes = [ctypes.c_void_p, c_int]
     L.nmfc_engine_kernel_flops.restype = ctypes.c_double
+    L.nmfc_brunet_default_opts.argtypes = [ctypes.POINTER(BrunetOpts)]
+    L.nmfc_brunet_default_opts.restype = None
+    L.nmfc_brunet_create.argtypes = [c_int, ctypes.c_void_p, c_int, c_int, c_int]
+    L.nmfc_brunet_create.restype = ctypes.c_void_p
+    L.nmfc_brunet_destroy.argtypes = [ctypes.c_void_p]
+    L.nmfc_brunet_destroy.restype = None
+    L.nmfc_brunet_run.argtypes = [ctypes.c_void_p, _ip, c_int, c_int, ctypes.POINTER(BrunetOpts), _dp, _dp,
+                                  ctypes.POINTER(Result)]
+    L.nmfc_brunet_run.restype = c_int
+    L.nmfc_brunet_set_timing.argtypes = [ctypes.c_void_p, c_int]
+    L.nmfc_brunet_set_timing.restype = None
+    L.nmfc_brunet_kernel_time.argtypes = [ctypes.c_void_p, c_int, _dp, _dp]
+    L.nmfc_brunet_kernel_time.restype = ctypes.c_longlong
     _LIB = L
     return L
 

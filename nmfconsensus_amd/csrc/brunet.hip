@@ -1,0 +1,750 @@
+// brunet.hip -- batched Brunet KL-divergence MU restarts (C ABI nmfc_brunet_* in include/nmfc.h).
+//
+// The per-restart algorithm is the BROAD nmfconsensus / GenePattern NMF.div (Brunet et al. 2004),
+// which the reference names at test_nmf.r:29 but does not ship (restated in
+// oracle/brunet_oracle.c, parity against the reference unpinned):
+//   VP = W H;  H <- (H * (W^T (A / VP)) + eps) / colSums(W)          (k_br_hnum + k_br_hupd)
+//   VP = W H;  W <- (W * ((A / VP) H^T) + eps) / rowSums(H)          (k_br_wupd)
+//   every stopfreq iterations: per-sample argmax class, stop after stopconv unchanged checks.
+// Init per restart: set.seed(seed + i); W <- runif(m k); H <- runif(k n) (R's Mersenne-Twister, k_br_init).
+//
+// The quotient A / VP is restart-specific, so the per-iteration work is 2 m n divides plus 8 m n k
+// flop of rank-k products per restart with nothing to share but A: these are VALU kernels (fp64 FMA
+// + IEEE divide, the divide dominating for small k), not MFMA GEMMs.  A is shared by streaming one A
+// element per lane and applying it to RG restarts at once; the per-restart W row (H-side) or H column
+// (W-side) is wave-uniform and comes through scalar loads, so no LDS staging and no cross-lane
+// reductions are needed.  Layouts (per k batch of B restarts):
+//   Arm [m][n_pad] (sample-contiguous rows), Acm [n][m_pad] (gene-contiguous columns)
+//   W   [B][m][K]  (gene-major, k contiguous)    H [B][n][K]  (= libnmf column-major k x n)
+//   Gp  [chunk][B][K][n_pad]  split-K partials of W^T (A / VP) over fixed gene chunks
+// Every sum's order depends only on (m, n, k): fixed gene chunks, fixed tree reductions, never on
+// the batch, the group a restart lands in or the GPU count.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nmfc.h"
+
+void nmfc_set_error(const char* msg);
+
+namespace {
+
+constexpr int BT = 256;
+constexpr int BR_KMAX = 16;
+constexpr double EPS = 2.220446049250313e-16;   // .Machine$double.eps
+
+void br_err(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+void br_err(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  nmfc_set_error(buf);
+}
+
+#define BCHECK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) {                                                                \
+      br_err("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return -1;                                                                           \
+    }                                                                                      \
+  } while (0)
+
+long rup(long v, long a) { return (v + a - 1) / a * a; }
+
+struct Buf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (need == 0) return 0;
+    hipError_t e = hipMalloc(&p, need);
+    if (e != hipSuccess) {
+      br_err("hipMalloc(%zu) failed: %s", need, hipGetErrorString(e));
+      p = nullptr;
+      return -1;
+    }
+    bytes = need;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+// restarts per workgroup group: each lane keeps 4K doubles of state per restart (H or W row in,
+// accumulator out), so small k shares every A element over more restarts
+constexpr int rg_of(int K) { return K <= 2 ? 8 : K <= 3 ? 6 : K <= 4 ? 5 : K <= 5 ? 4 : K <= 6 ? 3 : K <= 10 ? 2 : 1; }
+
+// ------------------------------------------------------------------------------------------------
+// Kernels
+// ------------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t mt_step(uint32_t cur, uint32_t nxt, uint32_t far) {
+  const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+  return far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// set.seed(seeds[b]); W <- matrix(runif(m*K), m, K); H <- matrix(runif(K*n), K, n)  (one workgroup per
+// restart).  The 624-word regeneration runs in four dependency phases: kk < 227 reads old words only;
+// 227 <= kk < 454 and 454 <= kk < 623 read kk - 227 from the previous phase; kk = 623 reads 0 and 396.
+__global__ __launch_bounds__(BT) void k_br_init(const uint32_t* __restrict__ seeds, int m, int n, int K,
+                                                double* __restrict__ W, long wstride, double* __restrict__ H,
+                                                long hstride) {
+  __shared__ uint32_t mt[624];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    uint32_t s = seeds[b];
+    for (int j = 0; j < 51; ++j) s = 69069u * s + 1u;   // 50 scrambling steps + the mti slot
+    for (int j = 0; j < 624; ++j) {
+      s = 69069u * s + 1u;
+      mt[j] = s;
+    }
+  }
+  __syncthreads();
+  const long nw = (long)m * K, total = nw + (long)K * n;
+  double* Wb = W + (long)b * wstride;
+  double* Hb = H + (long)b * hstride;
+  const int plo[4] = {0, 227, 454, 623}, phi[4] = {227, 454, 623, 624};
+  for (long base = 0; base < total; base += 624) {
+    for (int ph = 0; ph < 4; ++ph) {
+      const int kk = plo[ph] + tid;
+      const bool mine = kk < phi[ph];
+      uint32_t v = 0;
+      if (mine) v = mt_step(mt[kk], mt[kk == 623 ? 0 : kk + 1], mt[kk < 227 ? kk + 397 : kk - 227]);
+      __syncthreads();
+      if (mine) mt[kk] = v;
+      __syncthreads();
+    }
+    for (int t = tid; t < 624; t += BT) {
+      const long d = base + t;
+      if (d >= total) break;
+      uint32_t y = mt[t];
+      y ^= (y >> 11);
+      y ^= (y << 7) & 0x9d2c5680u;
+      y ^= (y << 15) & 0xefc60000u;
+      y ^= (y >> 18);
+      double u = (double)y * 2.3283064365386963e-10;
+      if (u <= 0.0) u = 0.5 * 2.328306437080797e-10;
+      else if (1.0 - u <= 0.0) u = 1.0 - 0.5 * 2.328306437080797e-10;
+      if (d < nw)
+        Wb[(d % m) * K + d / m] = u;
+      else
+        Hb[d - nw] = u;
+    }
+    __syncthreads();
+  }
+}
+
+// H side, split over fixed gene chunks: Gp[chunk][b][c][j] = sum_{i in chunk} W[b][i][c] * A[i][j] / VP[i][j],
+// VP[i][j] = sum_c W[b][i][c] H[b][j][c].  Lane = sample j; W rows are wave-uniform (scalar loads).
+template <int K, int RG>
+__global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, long n_pad, int m, int n, int gc,
+                                                const int* __restrict__ act, int nact, const double* __restrict__ W,
+                                                long wstride, const double* __restrict__ H, long hstride,
+                                                double* __restrict__ Gp, long gp_cs) {
+  const int j = blockIdx.x * BT + threadIdx.x;
+  const int jl = j < n ? j : n - 1;
+  const int chunk = blockIdx.y;
+  const int g0 = blockIdx.z * RG;
+  const int i0 = chunk * gc, i1 = min(m, i0 + gc);
+  int slot[RG];
+  double h[RG][K], g[RG][K];
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    slot[r] = act[min(g0 + r, nact - 1)];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      h[r][c] = H[(long)slot[r] * hstride + (long)jl * K + c];
+      g[r][c] = 0.0;
+    }
+  }
+  const double* ap = Arm + (long)i0 * n_pad + jl;
+#pragma unroll 2
+  for (int i = i0; i < i1; ++i, ap += n_pad) {
+    const double a = *ap;
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      if (g0 + r < nact) {
+        const double* wr = W + (long)slot[r] * wstride + (long)i * K;
+        double w[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) w[c] = wr[c];
+        double p = 0.0;
+#pragma unroll
+        for (int c = 0; c < K; ++c) p = fma(w[c], h[r][c], p);
+        const double q = a / p;
+#pragma unroll
+        for (int c = 0; c < K; ++c) g[r][c] = fma(w[c], q, g[r][c]);
+      }
+    }
+  }
+  if (j < n) {
+#pragma unroll
+    for (int r = 0; r < RG; ++r)
+      if (g0 + r < nact) {
+#pragma unroll
+        for (int c = 0; c < K; ++c) Gp[(long)chunk * gp_cs + ((long)slot[r] * K + c) * n_pad + j] = g[r][c];
+      }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void tree_sum(double (*red)[BT], double* v) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int c = 0; c < K; ++c) red[c][tid] = v[c];
+  __syncthreads();
+  for (int s = BT / 2; s > 0; s >>= 1) {
+    if (tid < s) {
+#pragma unroll
+      for (int c = 0; c < K; ++c) red[c][tid] += red[c][tid + s];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int c = 0; c < K; ++c) v[c] = red[c][0];
+  __syncthreads();
+}
+
+// One workgroup per live restart: colSums(W) (apply(W, 2, sum)), sum of the chunk partials,
+// H <- (H * G + eps) / colSums(W), rowSums(new H) for the W side, and on check iterations the
+// membership test (order(H[,j], decreasing = TRUE)[1] vs the previous check).
+template <int K>
+__global__ __launch_bounds__(BT) void k_br_hupd(int t, int check, int stopconv, int nchunks, int m, int n, long n_pad,
+                                                const int* __restrict__ act, const double* __restrict__ W, long wstride,
+                                                double* __restrict__ H, long hstride, const double* __restrict__ Gp,
+                                                long gp_cs, double* __restrict__ RS, int* __restrict__ memb,
+                                                int* __restrict__ nochange, int* __restrict__ stop_iter) {
+  __shared__ double red[K][BT];
+  const int b = act[blockIdx.x], tid = threadIdx.x;
+  double cs[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) cs[c] = 0.0;
+  const double* Wb = W + (long)b * wstride;
+  for (int i = tid; i < m; i += BT) {
+#pragma unroll
+    for (int c = 0; c < K; ++c) cs[c] += Wb[(long)i * K + c];
+  }
+  tree_sum<K>(red, cs);
+  double rs[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) rs[c] = 0.0;
+  int changed = 0;
+  double* Hb = H + (long)b * hstride;
+  for (int j = tid; j < n; j += BT) {
+    double hv[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const double* gp = Gp + ((long)b * K + c) * n_pad + j;
+      double g = 0.0;
+      for (int ch = 0; ch < nchunks; ++ch) g += gp[(long)ch * gp_cs];
+      hv[c] = __dadd_rn(__dmul_rn(Hb[(long)j * K + c], g), EPS) / cs[c];
+      Hb[(long)j * K + c] = hv[c];
+      rs[c] += hv[c];
+    }
+    if (check) {
+      int best = 0;
+#pragma unroll
+      for (int c = 1; c < K; ++c)
+        if (hv[c] > hv[best]) best = c;
+      const int mm = best + 1;
+      if (mm != memb[(long)b * n + j]) changed = 1;
+      memb[(long)b * n + j] = mm;
+    }
+  }
+  tree_sum<K>(red, rs);
+  if (tid == 0) {
+#pragma unroll
+    for (int c = 0; c < K; ++c) RS[(long)b * K + c] = rs[c];
+  }
+  if (check) {
+    const int any = __syncthreads_or(changed);
+    if (tid == 0) {
+      const int nc = any ? 0 : nochange[b] + 1;
+      nochange[b] = nc;
+      if (nc == stopconv) stop_iter[b] = t;
+    }
+  }
+}
+
+// W side: lane = gene i over every sample j: F[i][c] = sum_j A[i][j] / VP[i][j] * H[j][c] with the new H
+// (wave-uniform, scalar loads) and the old W row in registers; W <- (W * F + eps) / rowSums(H).
+template <int K, int RG>
+__global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, long m_pad, int m, int n,
+                                                const int* __restrict__ act, int nact, double* __restrict__ W,
+                                                long wstride, const double* __restrict__ H, long hstride,
+                                                const double* __restrict__ RS) {
+  const int i = blockIdx.x * BT + threadIdx.x;
+  const int il = i < m ? i : m - 1;
+  const int g0 = blockIdx.y * RG;
+  int slot[RG];
+  double w[RG][K], f[RG][K];
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    slot[r] = act[min(g0 + r, nact - 1)];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      w[r][c] = W[(long)slot[r] * wstride + (long)il * K + c];
+      f[r][c] = 0.0;
+    }
+  }
+  const double* ap = Acm + il;
+#pragma unroll 2
+  for (int j = 0; j < n; ++j, ap += m_pad) {
+    const double a = *ap;
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      if (g0 + r < nact) {
+        const double* hj = H + (long)slot[r] * hstride + (long)j * K;
+        double hh[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) hh[c] = hj[c];
+        double p = 0.0;
+#pragma unroll
+        for (int c = 0; c < K; ++c) p = fma(w[r][c], hh[c], p);
+        const double q = a / p;
+#pragma unroll
+        for (int c = 0; c < K; ++c) f[r][c] = fma(q, hh[c], f[r][c]);
+      }
+    }
+  }
+  if (i < m) {
+#pragma unroll
+    for (int r = 0; r < RG; ++r)
+      if (g0 + r < nact) {
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+          W[(long)slot[r] * wstride + (long)i * K + c] =
+              __dadd_rn(__dmul_rn(w[r][c], f[r][c]), EPS) / RS[(long)slot[r] * K + c];
+      }
+  }
+}
+
+// labels[b][j] = order(H[,j], decreasing = TRUE)[1] (first row of the column maximum, 1-based)
+__global__ __launch_bounds__(BT) void k_br_labels(const double* __restrict__ H, long hstride, int K, int n,
+                                                  int32_t* __restrict__ labels) {
+  const int b = blockIdx.y, j = blockIdx.x * BT + threadIdx.x;
+  if (j >= n) return;
+  const double* h = H + (long)b * hstride + (long)j * K;
+  int best = 0;
+  for (int c = 1; c < K; ++c)
+    if (h[c] > h[best]) best = c;
+  labels[(long)b * n + j] = best + 1;
+}
+
+// connect.matrix[i][j] = sum_b [labels_b(i) == labels_b(j)]   (exact integers)
+__global__ __launch_bounds__(BT) void k_br_counts(const int32_t* __restrict__ labels, int B, int n,
+                                                  int32_t* __restrict__ counts) {
+  const int i = blockIdx.x * 16 + (threadIdx.x & 15);
+  const int j = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (i >= n || j >= n) return;
+  int32_t cnt = 0;
+  for (int b = 0; b < B; ++b) cnt += labels[(long)b * n + i] == labels[(long)b * n + j];
+  counts[(long)j * n + i] = cnt;
+}
+
+__global__ void k_br_divide(const int32_t* __restrict__ counts, double denom, long len, double* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < len) out[i] = (double)counts[i] / denom;
+}
+
+__global__ void k_br_layout(const double* __restrict__ A, int m, int n, long m_pad, long n_pad,
+                            double* __restrict__ Acm, double* __restrict__ Arm) {
+  const int i = blockIdx.x * BT + threadIdx.x, j = blockIdx.y;
+  if (i >= m) return;
+  const double v = A[(long)j * m + i];
+  Acm[(long)j * m_pad + i] = v;
+  Arm[(long)i * n_pad + j] = v;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------------
+struct nmfc_brunet {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  int m = 0, n = 0;
+  long m_pad = 0, n_pad = 0;
+  int gc = 0, nchunks = 0;
+  Buf Acm, Arm, W, H, Gp, RS, memb, nochange, stop_iter, act, seeds, labels, counts_tmp, cons_tmp;
+  bool timing = false;
+  struct Pending {
+    int kid;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
+  double kms[3] = {0, 0, 0};
+  long long kcount[3] = {0, 0, 0};
+  double kfl_sum[3] = {0, 0, 0};
+};
+
+namespace {
+
+enum { BK_HNUM = 0, BK_HUPD = 1, BK_WUPD = 2 };
+
+hipEvent_t br_event(nmfc_brunet* e) {
+  if (!e->pool.empty()) {
+    hipEvent_t v = e->pool.back();
+    e->pool.pop_back();
+    return v;
+  }
+  hipEvent_t v = nullptr;
+  if (hipEventCreate(&v) != hipSuccess) return nullptr;
+  return v;
+}
+
+void br_drain(nmfc_brunet* e) {
+  for (auto& p : e->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) e->kms[p.kid] += ms;
+    e->pool.push_back(p.a);
+    e->pool.push_back(p.b);
+  }
+  e->pending.clear();
+}
+
+struct BTimed {
+  nmfc_brunet* e;
+  int kid;
+  hipEvent_t a = nullptr;
+  BTimed(nmfc_brunet* e_, int kid_, double flops) : e(e_), kid(kid_) {
+    e->kcount[kid] += 1;
+    e->kfl_sum[kid] += flops;
+    if (e->timing && (a = br_event(e))) (void)hipEventRecord(a, e->st);
+  }
+  ~BTimed() {
+    if (e->timing && a) {
+      hipEvent_t b = br_event(e);
+      if (b) {
+        (void)hipEventRecord(b, e->st);
+        e->pending.push_back({kid, a, b});
+      }
+    }
+  }
+};
+
+// one k: B restarts (slots 0..B-1) already initialised in e->W / e->H; iterates to the stop rule.
+template <int K>
+int br_iterate(nmfc_brunet* e, int B, const nmfc_brunet_opts& o, std::vector<int>& iters, std::vector<int>& stopped) {
+  constexpr int RG = rg_of(K);
+  const int m = e->m, n = e->n;
+  hipStream_t st = e->st;
+  const long wstride = (long)m * K, hstride = (long)n * K;
+  const long gp_cs = (long)B * K * e->n_pad;
+  std::vector<int> act(B), si(B, 0);
+  for (int b = 0; b < B; ++b) act[b] = b;
+  int nact = B;
+  BCHECK(hipMemcpyAsync(e->act.p, act.data(), sizeof(int) * B, hipMemcpyHostToDevice, st));
+  BCHECK(hipMemsetAsync(e->memb.p, 0, sizeof(int) * (size_t)B * n, st));   // old.membership starts at 0
+  BCHECK(hipMemsetAsync(e->nochange.p, 0, sizeof(int) * B, st));
+  BCHECK(hipMemsetAsync(e->stop_iter.p, 0, sizeof(int) * B, st));
+  const double fl = 4.0 * m * n * K;   // algorithmic flop per restart and kernel: VP (2mnk) + product (2mnk)
+  for (int t = 1; t <= o.maxiter && nact > 0; ++t) {
+    const int check = (t % o.stopfreq) == 0;
+    const int groups = (nact + RG - 1) / RG;
+    {
+      BTimed tl(e, BK_HNUM, fl * nact);
+      hipLaunchKernelGGL((k_br_hnum<K, RG>), dim3((n + BT - 1) / BT, e->nchunks, groups), dim3(BT), 0, st,
+                         e->Arm.as<double>(), e->n_pad, m, n, e->gc, e->act.as<int>(), nact, e->W.as<double>(), wstride,
+                         e->H.as<double>(), hstride, e->Gp.as<double>(), gp_cs);
+    }
+    {
+      BTimed tl(e, BK_HUPD, 0.0);
+      hipLaunchKernelGGL((k_br_hupd<K>), dim3(nact), dim3(BT), 0, st, t, check, o.stopconv, e->nchunks, m, n, e->n_pad,
+                         e->act.as<int>(), e->W.as<double>(), wstride, e->H.as<double>(), hstride, e->Gp.as<double>(),
+                         gp_cs, e->RS.as<double>(), e->memb.as<int>(), e->nochange.as<int>(), e->stop_iter.as<int>());
+    }
+    {
+      BTimed tl(e, BK_WUPD, fl * nact);
+      hipLaunchKernelGGL((k_br_wupd<K, RG>), dim3((m + BT - 1) / BT, groups), dim3(BT), 0, st, e->Acm.as<double>(),
+                         e->m_pad, m, n, e->act.as<int>(), nact, e->W.as<double>(), wstride, e->H.as<double>(), hstride,
+                         e->RS.as<double>());
+    }
+    BCHECK(hipGetLastError());
+    if (check) {
+      // stops happen only on check iterations, after that iteration's W update (NMF.div breaks at the
+      // end of the iteration): drop stopped restarts from the launch list
+      BCHECK(hipMemcpyAsync(si.data(), e->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+      BCHECK(hipStreamSynchronize(st));
+      if (e->timing) br_drain(e);
+      int q = 0;
+      for (int x = 0; x < nact; ++x)
+        if (si[act[x]] == 0) act[q++] = act[x];
+      if (q != nact) {
+        nact = q;
+        if (nact > 0) BCHECK(hipMemcpyAsync(e->act.p, act.data(), sizeof(int) * nact, hipMemcpyHostToDevice, st));
+        BCHECK(hipStreamSynchronize(st));
+      }
+    }
+  }
+  BCHECK(hipMemcpyAsync(si.data(), e->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+  BCHECK(hipStreamSynchronize(st));
+  if (e->timing) br_drain(e);
+  iters.resize(B);
+  stopped.resize(B);
+  for (int b = 0; b < B; ++b) {
+    iters[b] = si[b] ? si[b] : o.maxiter;   // NMF.div returns t: the break iteration, else maxniter
+    stopped[b] = si[b] != 0;
+  }
+  return 0;
+}
+
+int br_dispatch(nmfc_brunet* e, int K, int B, const nmfc_brunet_opts& o, std::vector<int>& iters, std::vector<int>& stopped) {
+  switch (K) {
+#define BR_CASE(KK) \
+  case KK:          \
+    return br_iterate<KK>(e, B, o, iters, stopped);
+    BR_CASE(2) BR_CASE(3) BR_CASE(4) BR_CASE(5) BR_CASE(6) BR_CASE(7) BR_CASE(8) BR_CASE(9) BR_CASE(10) BR_CASE(11)
+    BR_CASE(12) BR_CASE(13) BR_CASE(14) BR_CASE(15) BR_CASE(16)
+#undef BR_CASE
+    default:
+      br_err("nmfc_brunet_run: k=%d unsupported", K);
+      return -1;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void nmfc_brunet_default_opts(nmfc_brunet_opts* o) {
+  memset(o, 0, sizeof *o);
+  o->maxiter = 2000;        // NMF.div maxniter
+  o->stopconv = 40;         // nmfconsensus stopconv
+  o->stopfreq = 10;         // nmfconsensus stopfreq
+  o->seed = 123456789u;     // nmfconsensus rseed
+  o->restart_begin = 0;
+  o->restart_end = -1;
+  o->verbose = 0;
+}
+
+nmfc_brunet* nmfc_brunet_create(int device, const double* A, int m, int n, int a_on_device) {
+  if (!A || m <= 0 || n <= 0) {
+    br_err("nmfc_brunet_create: bad arguments (A=%p m=%d n=%d)", (const void*)A, m, n);
+    return nullptr;
+  }
+  nmfc_brunet* e = new nmfc_brunet();
+  auto fail = [&](const char* what, hipError_t err) -> nmfc_brunet* {
+    br_err("nmfc_brunet_create: %s: %s", what, hipGetErrorString(err));
+    nmfc_brunet_destroy(e);
+    return nullptr;
+  };
+  hipError_t err;
+  if (device >= 0 && (err = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", err);
+  if ((err = hipGetDevice(&e->dev)) != hipSuccess) return fail("hipGetDevice", err);
+  if ((err = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", err);
+  e->m = m;
+  e->n = n;
+  e->m_pad = rup(m, BT);
+  e->n_pad = rup(n, BT);
+  // fixed gene chunks (a function of m only): about 16 chunks of whole wavefronts, at most 2048 genes
+  e->gc = (int)std::min<long>(2048, std::max<long>(64, rup((m + 15) / 16, 64)));
+  e->nchunks = (m + e->gc - 1) / e->gc;
+  if (e->Acm.ensure(sizeof(double) * e->m_pad * n) || e->Arm.ensure(sizeof(double) * (size_t)m * e->n_pad)) {
+    nmfc_brunet_destroy(e);
+    return nullptr;
+  }
+  if ((err = hipMemsetAsync(e->Acm.p, 0, e->Acm.bytes, e->st)) != hipSuccess) return fail("memset", err);
+  if ((err = hipMemsetAsync(e->Arm.p, 0, e->Arm.bytes, e->st)) != hipSuccess) return fail("memset", err);
+  const double* dA = A;
+  Buf tmp;
+  if (!a_on_device) {
+    if (tmp.ensure(sizeof(double) * (size_t)m * n)) {
+      nmfc_brunet_destroy(e);
+      return nullptr;
+    }
+    if ((err = hipMemcpyAsync(tmp.p, A, sizeof(double) * (size_t)m * n, hipMemcpyHostToDevice, e->st)) != hipSuccess)
+      return fail("upload A", err);
+    dA = tmp.as<double>();
+  }
+  hipLaunchKernelGGL(k_br_layout, dim3((m + BT - 1) / BT, n), dim3(BT), 0, e->st, dA, m, n, e->m_pad, e->n_pad,
+                     e->Acm.as<double>(), e->Arm.as<double>());
+  if ((err = hipGetLastError()) != hipSuccess) return fail("k_br_layout", err);
+  if ((err = hipStreamSynchronize(e->st)) != hipSuccess) return fail("sync", err);
+  tmp.release();
+  return e;
+}
+
+void nmfc_brunet_destroy(nmfc_brunet* e) {
+  if (!e) return;
+  if (e->st) (void)hipStreamSynchronize(e->st);
+  br_drain(e);
+  for (auto v : e->pool) (void)hipEventDestroy(v);
+  Buf* bufs[] = {&e->Acm, &e->Arm,      &e->W,         &e->H,   &e->Gp,    &e->RS,     &e->memb,
+                 &e->nochange, &e->stop_iter, &e->act, &e->seeds, &e->labels, &e->counts_tmp, &e->cons_tmp};
+  for (Buf* b : bufs) b->release();
+  if (e->st) (void)hipStreamDestroy(e->st);
+  delete e;
+}
+
+void nmfc_brunet_set_timing(nmfc_brunet* e, int enable) {
+  if (e) e->timing = enable != 0;
+}
+
+long long nmfc_brunet_kernel_time(nmfc_brunet* e, int kid, double* ms_out, double* flops_per_launch) {
+  if (!e || kid < 0 || kid > 2) return -1;
+  if (ms_out) *ms_out = e->kms[kid];
+  if (flops_per_launch) *flops_per_launch = e->kcount[kid] ? e->kfl_sum[kid] / e->kcount[kid] : 0.0;
+  return e->kcount[kid];
+}
+
+int nmfc_brunet_run(nmfc_brunet* e, const int* ks, int nk, int R, const nmfc_brunet_opts* opts_in,
+                    const double* W_init, const double* H_init, nmfc_result* out) {
+  if (!e || !ks || nk <= 0 || R <= 0) {
+    br_err("nmfc_brunet_run: bad arguments");
+    return -1;
+  }
+  nmfc_brunet_opts o;
+  if (opts_in)
+    o = *opts_in;
+  else
+    nmfc_brunet_default_opts(&o);
+  const int m = e->m, n = e->n;
+  if (o.maxiter < 1 || o.stopfreq < 1 || o.stopconv < 1) {
+    br_err("nmfc_brunet_run: maxiter, stopfreq and stopconv must be >= 1");
+    return -1;
+  }
+  for (int q = 0; q < nk; ++q)
+    if (ks[q] < 2 || ks[q] > BR_KMAX) {
+      br_err("nmfc_brunet_run: k=%d unsupported (need 2 <= k <= %d)", ks[q], BR_KMAX);
+      return -1;
+    }
+  const int rb = std::max(0, o.restart_begin);
+  const int re = o.restart_end < 0 ? R : std::min(o.restart_end, R);
+  if (rb >= re) {
+    br_err("nmfc_brunet_run: empty restart range [%d, %d)", rb, re);
+    return -1;
+  }
+  const int B = re - rb;
+  BCHECK(hipSetDevice(e->dev));
+  auto t0 = std::chrono::steady_clock::now();
+  for (int q = 0; q < 3; ++q) e->kms[q] = 0, e->kcount[q] = 0, e->kfl_sum[q] = 0;
+  int kmax = 0;
+  for (int q = 0; q < nk; ++q) kmax = std::max(kmax, ks[q]);
+  if (e->W.ensure(sizeof(double) * (size_t)B * m * kmax) || e->H.ensure(sizeof(double) * (size_t)B * n * kmax) ||
+      e->Gp.ensure(sizeof(double) * (size_t)e->nchunks * B * kmax * e->n_pad) ||
+      e->RS.ensure(sizeof(double) * (size_t)B * kmax) || e->memb.ensure(sizeof(int) * (size_t)B * n) ||
+      e->nochange.ensure(sizeof(int) * B) || e->stop_iter.ensure(sizeof(int) * B) || e->act.ensure(sizeof(int) * B) ||
+      e->seeds.ensure(sizeof(uint32_t) * B) || e->labels.ensure(sizeof(int32_t) * (size_t)B * n))
+    return -1;
+  hipStream_t st = e->st;
+  std::vector<uint32_t> seeds(B);
+  for (int b = 0; b < B; ++b) seeds[b] = o.seed + (uint32_t)(rb + b + 1);   // set.seed(rseed + i), i 1-based
+  BCHECK(hipMemcpyAsync(e->seeds.p, seeds.data(), sizeof(uint32_t) * B, hipMemcpyHostToDevice, st));
+  int32_t* dcounts = nullptr;
+  const size_t nn = (size_t)n * n;
+  if (out && (out->counts || out->consensus)) {
+    if (out->counts && out->counts_on_device) {
+      dcounts = out->counts;
+    } else {
+      if (e->counts_tmp.ensure(sizeof(int32_t) * nn * nk)) return -1;
+      dcounts = e->counts_tmp.as<int32_t>();
+    }
+  }
+  long long tot_iters = 0;
+  int max_it = 0;
+  double t_iter = 0.0;
+  long woff = 0, hoff = 0;
+  std::vector<double> hw, hh;
+  for (int ki = 0; ki < nk; ++ki) {
+    const int K = ks[ki];
+    const long wstride = (long)m * K, hstride = (long)n * K;
+    if (W_init && H_init) {
+      // caller factors for this k's B jobs: W_b m x K column-major, H_b K x n column-major
+      hw.assign((size_t)B * m * K, 0.0);
+      for (int b = 0; b < B; ++b)
+        for (int c = 0; c < K; ++c)
+          for (int i = 0; i < m; ++i) hw[(size_t)b * wstride + (size_t)i * K + c] = W_init[woff + (long)b * wstride + (long)c * m + i];
+      BCHECK(hipMemcpyAsync(e->W.p, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st));
+      BCHECK(hipMemcpyAsync(e->H.p, H_init + hoff, sizeof(double) * (size_t)B * hstride, hipMemcpyHostToDevice, st));
+      BCHECK(hipStreamSynchronize(st));
+    } else {
+      hipLaunchKernelGGL(k_br_init, dim3(B), dim3(BT), 0, st, e->seeds.as<uint32_t>(), m, n, K, e->W.as<double>(), wstride,
+                         e->H.as<double>(), hstride);
+      BCHECK(hipGetLastError());
+    }
+    std::vector<int> iters, stopped;
+    auto ti0 = std::chrono::steady_clock::now();
+    if (br_dispatch(e, K, B, o, iters, stopped)) return -1;
+    t_iter += std::chrono::duration<double>(std::chrono::steady_clock::now() - ti0).count();
+    hipLaunchKernelGGL(k_br_labels, dim3((n + BT - 1) / BT, B), dim3(BT), 0, st, e->H.as<double>(), hstride, K, n,
+                       e->labels.as<int32_t>());
+    BCHECK(hipGetLastError());
+    if (dcounts) {
+      hipLaunchKernelGGL(k_br_counts, dim3((n + 15) / 16, (n + 15) / 16), dim3(BT), 0, st, e->labels.as<int32_t>(), B, n,
+                         dcounts + nn * ki);
+      BCHECK(hipGetLastError());
+    }
+    if (out && out->labels)
+      BCHECK(hipMemcpyAsync(out->labels + (size_t)ki * B * n, e->labels.p, sizeof(int32_t) * (size_t)B * n,
+                            hipMemcpyDeviceToHost, st));
+    if (out && (out->W || out->H)) {
+      hw.resize((size_t)B * wstride);
+      hh.resize((size_t)B * hstride);
+      BCHECK(hipMemcpyAsync(hw.data(), e->W.p, sizeof(double) * hw.size(), hipMemcpyDeviceToHost, st));
+      BCHECK(hipMemcpyAsync(hh.data(), e->H.p, sizeof(double) * hh.size(), hipMemcpyDeviceToHost, st));
+      BCHECK(hipStreamSynchronize(st));
+      if (out->W)
+        for (int b = 0; b < B; ++b)
+          for (int c = 0; c < K; ++c)
+            for (int i = 0; i < m; ++i) out->W[woff + (long)b * wstride + (long)c * m + i] = hw[(size_t)b * wstride + (size_t)i * K + c];
+      if (out->H) memcpy(out->H + hoff, hh.data(), sizeof(double) * hh.size());
+    }
+    BCHECK(hipStreamSynchronize(st));
+    for (int b = 0; b < B; ++b) {
+      tot_iters += iters[b];
+      max_it = std::max(max_it, iters[b]);
+      if (out && out->iters) out->iters[(size_t)ki * B + b] = iters[b];
+      if (out && out->stopped_early) out->stopped_early[(size_t)ki * B + b] = stopped[b];
+    }
+    woff += (long)B * wstride;
+    hoff += (long)B * hstride;
+  }
+  if (out && dcounts) {
+    if (out->consensus) {
+      if (e->cons_tmp.ensure(sizeof(double) * nn * nk)) return -1;
+      hipLaunchKernelGGL(k_br_divide, dim3((unsigned)((nn * nk + BT - 1) / BT)), dim3(BT), 0, st, dcounts, (double)R,
+                         (long)(nn * nk), e->cons_tmp.as<double>());
+      BCHECK(hipGetLastError());
+      BCHECK(hipMemcpyAsync(out->consensus, e->cons_tmp.p, sizeof(double) * nn * nk, hipMemcpyDeviceToHost, st));
+    }
+    if (out->counts && !out->counts_on_device)
+      BCHECK(hipMemcpyAsync(out->counts, dcounts, sizeof(int32_t) * nn * nk, hipMemcpyDeviceToHost, st));
+  }
+  BCHECK(hipStreamSynchronize(st));
+  if (e->timing) br_drain(e);
+  auto t1 = std::chrono::steady_clock::now();
+  if (out) {
+    out->seconds_total = std::chrono::duration<double>(t1 - t0).count();
+    out->seconds_iterate = t_iter;
+    out->restart_iterations = tot_iters;
+    out->max_iter_run = max_it;
+  }
+  if (o.verbose)
+    fprintf(stderr, "[nmfc brunet] %d restarts x %d k, mean iters %.1f, max %d, %.3f s\n", B, nk,
+            (double)tot_iters / ((double)B * nk), max_it, std::chrono::duration<double>(t1 - t0).count());
+  return 0;
+}
+
+}  // extern "C"

@@ -169,6 +169,9 @@ Packing pack(const std::vector<RestartInfo>& in) {
 
 }  // namespace
 
+// error slot shared with the other translation units of the library (brunet.hip)
+__attribute__((visibility("hidden"))) void nmfc_set_error(const char* msg) { g_err = msg; }
+
 struct nmfc_engine {
   int dev = 0;
   hipStream_t st = nullptr;

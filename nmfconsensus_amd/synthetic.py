@@ -20,6 +20,8 @@ CONFIGS = {
     "C2": (1000, 40, list(range(2, 9)), 100, "synthetic 1000x40 fp64, k=2..8, 100 restarts"),
     "C3": (20000, 500, list(range(2, 11)), 200, "synthetic 20000x500 fp64, k=2..10, 200 restarts"),
     "C4": (60000, 2000, list(range(2, 16)), 1000, "synthetic 60000x2000 fp64, k=2..15, 1000 restarts"),
+    # BASELINE configs[4]: the Brunet KL-divergence MU variant (nmfc_brunet_*, nmfconsensus_amd/brunet.py)
+    "C5": (20000, 500, list(range(2, 11)), 200, "Brunet KL-divergence MU, synthetic 20000x500 fp64, k=2..10, 200 restarts"),
 }
 
 

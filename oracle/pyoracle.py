@@ -38,8 +38,13 @@ class _RandState(ctypes.Structure):
     _fields_ = [("ring", ctypes.c_uint32 * 34), ("pos", ctypes.c_uint64)]
 
 
+class _RMTState(ctypes.Structure):
+    _fields_ = [("mt", ctypes.c_uint32 * 624), ("mti", ctypes.c_int)]
+
+
 class Oracle:
-    """Restatement (port) of libnmf nmf_mu + init stream + consensus (nmf_oracle.c)."""
+    """Restatement (port) of libnmf nmf_mu + init stream + consensus (nmf_oracle.c), and of the
+    Brunet KL-divergence MU with R's set.seed/runif init (brunet_oracle.c)."""
 
     def __init__(self, path: str = ORACLE_SO):
         if not os.path.exists(path):
@@ -57,7 +62,39 @@ class Oracle:
         L.orc_calculate_norm.restype = ctypes.c_double
         L.orc_calculate_maxchange.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_double]
         L.orc_calculate_maxchange.restype = ctypes.c_double
+        # Brunet KL-divergence MU (brunet_oracle.c; parity unpinned vs the reference, see its header)
+        L.orc_rmt_seed.argtypes = [ctypes.POINTER(_RMTState), ctypes.c_uint32]
+        L.orc_rmt_unif.argtypes = [ctypes.POINTER(_RMTState)]
+        L.orc_rmt_unif.restype = ctypes.c_double
+        L.orc_brunet_init.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp]
+        L.orc_brunet.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_void_p]
+        L.orc_brunet.restype = ctypes.c_int
         self.L = L
+
+    def runif(self, seed: int, count: int) -> np.ndarray:
+        """set.seed(seed); runif(count) (R's Mersenne-Twister restated)."""
+        st = _RMTState()
+        self.L.orc_rmt_seed(ctypes.byref(st), seed & 0xFFFFFFFF)
+        return np.array([self.L.orc_rmt_unif(ctypes.byref(st)) for _ in range(count)], dtype=np.float64)
+
+    def brunet_init(self, seed: int, m: int, n: int, k: int):
+        W = np.zeros((m, k), dtype=np.float64, order="F")
+        H = np.zeros((k, n), dtype=np.float64, order="F")
+        self.L.orc_brunet_init(seed & 0xFFFFFFFF, m, n, k, _d(W), _d(H))
+        return W, H
+
+    def brunet(self, A, W, H, maxiter: int, stopconv: int = 40, stopfreq: int = 10, want_error: bool = False):
+        """NMF.div (Brunet KL MU) -> (W, H, t[, error.v])."""
+        A = np.asfortranarray(A, dtype=np.float64)
+        W = np.array(W, dtype=np.float64, order="F", copy=True)
+        H = np.array(H, dtype=np.float64, order="F", copy=True)
+        m, n = A.shape
+        k = W.shape[1]
+        err = np.zeros(maxiter, dtype=np.float64) if want_error else None
+        t = self.L.orc_brunet(_d(A), _d(W), _d(H), m, n, k, maxiter, stopconv, stopfreq,
+                              err.ctypes.data_as(ctypes.c_void_p) if want_error else None)
+        return (W, H, t, err[:t]) if want_error else (W, H, t)
 
     def rand_stream(self, seed: int, count: int) -> np.ndarray:
         st = _RandState()
