@@ -116,6 +116,7 @@ typedef struct nmfc_brunet_opts {
   int restart_begin;  /* shard [restart_begin, restart_end) of the restarts 0..R-1, for every k; end < 0 => R */
   int restart_end;
   int verbose;
+  int lanes;          /* k batches run concurrently, each on its own HIP stream (0 = default 4, max 4) */
 } nmfc_brunet_opts;
 
 typedef struct nmfc_brunet nmfc_brunet;

@@ -35,7 +35,7 @@ class Result(ctypes.Structure):
 
 class BrunetOpts(ctypes.Structure):
     _fields_ = [("maxiter", c_int), ("stopconv", c_int), ("stopfreq", c_int), ("seed", ctypes.c_uint32),
-                ("restart_begin", c_int), ("restart_end", c_int), ("verbose", c_int)]
+                ("restart_begin", c_int), ("restart_end", c_int), ("verbose", c_int), ("lanes", c_int)]
 
 
 BK_HNUM, BK_HUPD, BK_WUPD = 0, 1, 2

@@ -79,7 +79,8 @@ class BrunetEngine:
 
     def run(self, ks, R: int, *, maxiter: int = 2000, seed: int = 123456789, stopconv: int = 40, stopfreq: int = 10,
             restart_begin: int = 0, restart_end: int = -1, W_init=None, H_init=None, want_factors: bool = False,
-            want_counts: bool = True, counts_device_ptr: int | None = None, verbose: bool = False) -> SweepResult:
+            want_counts: bool = True, counts_device_ptr: int | None = None, verbose: bool = False,
+            lanes: int = 0) -> SweepResult:
         """Jobs in nmfconsensus order (for k in ks: for i in restart shard); per-job arrays follow it."""
         ks = [int(k) for k in ks]
         nk = len(ks)
@@ -93,7 +94,7 @@ class BrunetEngine:
         o = BrunetOpts()
         self.L.nmfc_brunet_default_opts(ctypes.byref(o))
         o.maxiter, o.stopconv, o.stopfreq, o.seed = maxiter, stopconv, stopfreq, seed & 0xFFFFFFFF
-        o.restart_begin, o.restart_end, o.verbose = rb, re, 1 if verbose else 0
+        o.restart_begin, o.restart_end, o.verbose, o.lanes = rb, re, 1 if verbose else 0, lanes
         m, n = self.m, self.n
         res = Result()
         iters = np.zeros(nj, dtype=np.int32)

@@ -22,11 +22,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/nmfc.h"
@@ -91,6 +95,25 @@ struct Buf {
 
 // restarts per workgroup group: each lane keeps 4K doubles of state per restart (H or W row in,
 // accumulator out), so small k shares every A element over more restarts
+// q = a / p: rcp + two Newton steps + one residual correction (Markstein's final step), i.e. the
+// compiler's IEEE sequence without its operand-scaling steps (div_scale / div_fmas / div_fixup), which
+// only matter near the exponent limits.  Here a >= 0 and p is a positive rank-k product of
+// [eps, O(1)]-scaled factors; parity to the IEEE-divide oracle is unchanged (tests/test_gpu_brunet.py),
+// and the kernels issue ~10 % fewer VALU cycles per quotient.  NMFC_BRUNET_IEEEDIV restores '/'.
+__device__ __forceinline__ double quot(double a, double p) {
+#ifdef NMFC_BRUNET_IEEEDIV
+  return a / p;
+#else
+  double r = __builtin_amdgcn_rcp(p);
+  double e = fma(-p, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-p, r, 1.0);
+  r = fma(r, e, r);
+  const double q = a * r;
+  return fma(fma(-p, q, a), r, q);
+#endif
+}
+
 constexpr int rg_of(int K) { return K <= 2 ? 8 : K <= 3 ? 6 : K <= 4 ? 5 : K <= 5 ? 4 : K <= 6 ? 3 : K <= 10 ? 2 : 1; }
 
 // ------------------------------------------------------------------------------------------------
@@ -153,55 +176,113 @@ __global__ __launch_bounds__(BT) void k_br_init(const uint32_t* __restrict__ see
   }
 }
 
+// Tile of the wave-uniform operand (W rows of the H side, H columns of the W side) for the RG
+// restarts of a workgroup: TL consecutive gene (sample) rows of K doubles per restart, contiguous in
+// HBM, fetched with coalesced vector loads one tile ahead into registers and stored into the other
+// half of a double-buffered LDS array; the inner loop reads it back with broadcast LDS reads.
+constexpr int TL = 64;
+// inner-loop unroll per k (measured, tools/brunet_kbench.py: unroll 4 is faster for most k, unroll 2
+// where the unrolled live ranges push the register count past an occupancy step)
+constexpr int br_unroll(int K) { return (K == 5 || K == 7 || K == 10) ? 2 : 4; }
+
+template <int K, int RG>
+struct OperandTiles {
+  static constexpr int TW = RG * TL * K;              // doubles per tile (all restarts)
+  static constexpr int PER = (TW + BT - 1) / BT;      // per thread
+  double pre[PER];
+  // rows [t0, t0 + TL) of X[slot_r][row][c] (row stride K), rows >= rows_end read as 0
+  __device__ __forceinline__ void fetch(const double* __restrict__ X, long stride, const int* sl, int t0,
+                                        int rows_end) {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int idx = threadIdx.x + e * BT;
+      double v = 0.0;
+      if (idx < TW) {
+        const int r = idx / (TL * K), rem = idx - r * (TL * K);
+        if (rem < (rows_end - t0) * K) v = X[(long)sl[r] * stride + (long)t0 * K + rem];
+      }
+      pre[e] = v;
+    }
+  }
+  __device__ __forceinline__ void store(double* lds) {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int idx = threadIdx.x + e * BT;
+      if (idx < TW) lds[idx] = pre[e];
+    }
+  }
+};
+
 // H side, split over fixed gene chunks: Gp[chunk][b][c][j] = sum_{i in chunk} W[b][i][c] * A[i][j] / VP[i][j],
-// VP[i][j] = sum_c W[b][i][c] H[b][j][c].  Lane = sample j; W rows are wave-uniform (scalar loads).
+// VP[i][j] = sum_c W[b][i][c] H[b][j][c].  Lane = sample j (H column and accumulator in registers);
+// W rows through the double-buffered LDS tiles.
 template <int K, int RG>
 __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, long n_pad, int m, int n, int gc,
                                                 const int* __restrict__ act, int nact, const double* __restrict__ W,
                                                 long wstride, const double* __restrict__ H, long hstride,
                                                 double* __restrict__ Gp, long gp_cs) {
+  using OT = OperandTiles<K, RG>;
+  __shared__ double wl[2][OT::TW];
+  __shared__ int sl[RG];
   const int j = blockIdx.x * BT + threadIdx.x;
   const int jl = j < n ? j : n - 1;
   const int chunk = blockIdx.y;
   const int g0 = blockIdx.z * RG;
+  const int nlive = min(RG, nact - g0);
   const int i0 = chunk * gc, i1 = min(m, i0 + gc);
-  int slot[RG];
+  if (threadIdx.x < RG) sl[threadIdx.x] = act[min(g0 + (int)threadIdx.x, nact - 1)];
+  __syncthreads();
   double h[RG][K], g[RG][K];
 #pragma unroll
   for (int r = 0; r < RG; ++r) {
-    slot[r] = act[min(g0 + r, nact - 1)];
 #pragma unroll
     for (int c = 0; c < K; ++c) {
-      h[r][c] = H[(long)slot[r] * hstride + (long)jl * K + c];
+      h[r][c] = H[(long)sl[r] * hstride + (long)jl * K + c];
       g[r][c] = 0.0;
     }
   }
-  const double* ap = Arm + (long)i0 * n_pad + jl;
-#pragma unroll 2
-  for (int i = i0; i < i1; ++i, ap += n_pad) {
-    const double a = *ap;
+  OT ot;
+  ot.fetch(W, wstride, sl, i0, i1);
+  ot.store(wl[0]);
+  __syncthreads();
+  int buf = 0;
+  for (int t0 = i0; t0 < i1; t0 += TL, buf ^= 1) {
+    const bool more = t0 + TL < i1;
+    if (more) ot.fetch(W, wstride, sl, t0 + TL, i1);
+    const double* ap = Arm + (long)t0 * n_pad + jl;
+    const double* wt = wl[buf];
+    // slots past the live restarts repeat the last live one (computed, never stored): no branches here
+    auto gene = [&](int ii) {
+      const double a = ap[(long)ii * n_pad];
 #pragma unroll
-    for (int r = 0; r < RG; ++r) {
-      if (g0 + r < nact) {
-        const double* wr = W + (long)slot[r] * wstride + (long)i * K;
+      for (int r = 0; r < RG; ++r) {
+        const double* wr = wt + r * (TL * K) + ii * K;
         double w[K];
 #pragma unroll
         for (int c = 0; c < K; ++c) w[c] = wr[c];
         double p = 0.0;
 #pragma unroll
         for (int c = 0; c < K; ++c) p = fma(w[c], h[r][c], p);
-        const double q = a / p;
+        const double q = quot(a, p);
 #pragma unroll
         for (int c = 0; c < K; ++c) g[r][c] = fma(w[c], q, g[r][c]);
       }
+    };
+    if (i1 - t0 >= TL) {
+#pragma unroll br_unroll(K)
+      for (int ii = 0; ii < TL; ++ii) gene(ii);
+    } else {
+      for (int ii = 0; ii < i1 - t0; ++ii) gene(ii);
     }
+    if (more) ot.store(wl[buf ^ 1]);
+    __syncthreads();
   }
   if (j < n) {
 #pragma unroll
     for (int r = 0; r < RG; ++r)
-      if (g0 + r < nact) {
+      if (r < nlive) {
 #pragma unroll
-        for (int c = 0; c < K; ++c) Gp[(long)chunk * gp_cs + ((long)slot[r] * K + c) * n_pad + j] = g[r][c];
+        for (int c = 0; c < K; ++c) Gp[(long)chunk * gp_cs + ((long)sl[r] * K + c) * n_pad + j] = g[r][c];
       }
   }
 }
@@ -286,54 +367,73 @@ __global__ __launch_bounds__(BT) void k_br_hupd(int t, int check, int stopconv, 
 }
 
 // W side: lane = gene i over every sample j: F[i][c] = sum_j A[i][j] / VP[i][j] * H[j][c] with the new H
-// (wave-uniform, scalar loads) and the old W row in registers; W <- (W * F + eps) / rowSums(H).
+// (LDS tiles of TL samples) and the old W row in registers; W <- (W * F + eps) / rowSums(H).
 template <int K, int RG>
 __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, long m_pad, int m, int n,
                                                 const int* __restrict__ act, int nact, double* __restrict__ W,
                                                 long wstride, const double* __restrict__ H, long hstride,
                                                 const double* __restrict__ RS) {
+  using OT = OperandTiles<K, RG>;
+  __shared__ double hl[2][OT::TW];
+  __shared__ int sl[RG];
   const int i = blockIdx.x * BT + threadIdx.x;
   const int il = i < m ? i : m - 1;
   const int g0 = blockIdx.y * RG;
-  int slot[RG];
+  const int nlive = min(RG, nact - g0);
+  if (threadIdx.x < RG) sl[threadIdx.x] = act[min(g0 + (int)threadIdx.x, nact - 1)];
+  __syncthreads();
   double w[RG][K], f[RG][K];
 #pragma unroll
   for (int r = 0; r < RG; ++r) {
-    slot[r] = act[min(g0 + r, nact - 1)];
 #pragma unroll
     for (int c = 0; c < K; ++c) {
-      w[r][c] = W[(long)slot[r] * wstride + (long)il * K + c];
+      w[r][c] = W[(long)sl[r] * wstride + (long)il * K + c];
       f[r][c] = 0.0;
     }
   }
-  const double* ap = Acm + il;
-#pragma unroll 2
-  for (int j = 0; j < n; ++j, ap += m_pad) {
-    const double a = *ap;
+  OT ot;
+  ot.fetch(H, hstride, sl, 0, n);
+  ot.store(hl[0]);
+  __syncthreads();
+  int buf = 0;
+  for (int s0 = 0; s0 < n; s0 += TL, buf ^= 1) {
+    const bool more = s0 + TL < n;
+    if (more) ot.fetch(H, hstride, sl, s0 + TL, n);
+    const double* ap = Acm + (long)s0 * m_pad + il;
+    const double* ht = hl[buf];
+    auto sample = [&](int jj) {
+      const double a = ap[(long)jj * m_pad];
 #pragma unroll
-    for (int r = 0; r < RG; ++r) {
-      if (g0 + r < nact) {
-        const double* hj = H + (long)slot[r] * hstride + (long)j * K;
+      for (int r = 0; r < RG; ++r) {
+        const double* hj = ht + r * (TL * K) + jj * K;
         double hh[K];
 #pragma unroll
         for (int c = 0; c < K; ++c) hh[c] = hj[c];
         double p = 0.0;
 #pragma unroll
         for (int c = 0; c < K; ++c) p = fma(w[r][c], hh[c], p);
-        const double q = a / p;
+        const double q = quot(a, p);
 #pragma unroll
         for (int c = 0; c < K; ++c) f[r][c] = fma(q, hh[c], f[r][c]);
       }
+    };
+    if (n - s0 >= TL) {
+#pragma unroll br_unroll(K)
+      for (int jj = 0; jj < TL; ++jj) sample(jj);
+    } else {
+      for (int jj = 0; jj < n - s0; ++jj) sample(jj);
     }
+    if (more) ot.store(hl[buf ^ 1]);
+    __syncthreads();
   }
   if (i < m) {
 #pragma unroll
     for (int r = 0; r < RG; ++r)
-      if (g0 + r < nact) {
+      if (r < nlive) {
 #pragma unroll
         for (int c = 0; c < K; ++c)
-          W[(long)slot[r] * wstride + (long)i * K + c] =
-              __dadd_rn(__dmul_rn(w[r][c], f[r][c]), EPS) / RS[(long)slot[r] * K + c];
+          W[(long)sl[r] * wstride + (long)i * K + c] =
+              __dadd_rn(__dmul_rn(w[r][c], f[r][c]), EPS) / RS[(long)sl[r] * K + c];
       }
   }
 }
@@ -378,15 +478,18 @@ __global__ void k_br_layout(const double* __restrict__ A, int m, int n, long m_p
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
-// Host side
+// Host side.  Each k is one batch of B restarts run by a "lane" (own HIP stream and buffers); up to
+// BR_LANES lanes run concurrently from a small host thread pool, largest k first, so that the small
+// grids of a batch's last stragglers overlap with the other ranks' batches instead of idling the chip.
 // ------------------------------------------------------------------------------------------------
-struct nmfc_brunet {
-  int dev = 0;
+namespace {
+
+constexpr int BR_LANES = 4;   // = the HW queues HIP gives a process by default (GPU_MAX_HW_QUEUES)
+enum { BK_HNUM = 0, BK_HUPD = 1, BK_WUPD = 2 };
+
+struct BrLane {
   hipStream_t st = nullptr;
-  int m = 0, n = 0;
-  long m_pad = 0, n_pad = 0;
-  int gc = 0, nchunks = 0;
-  Buf Acm, Arm, W, H, Gp, RS, memb, nochange, stop_iter, act, seeds, labels, counts_tmp, cons_tmp;
+  Buf W, H, Gp, RS, memb, nochange, stop_iter, act, seeds, labels;
   bool timing = false;
   struct Pending {
     int kid;
@@ -397,16 +500,20 @@ struct nmfc_brunet {
   double kms[3] = {0, 0, 0};
   long long kcount[3] = {0, 0, 0};
   double kfl_sum[3] = {0, 0, 0};
+  void release() {
+    Buf* bufs[] = {&W, &H, &Gp, &RS, &memb, &nochange, &stop_iter, &act, &seeds, &labels};
+    for (Buf* b : bufs) b->release();
+    for (auto v : pool) (void)hipEventDestroy(v);
+    pool.clear();
+    if (st) (void)hipStreamDestroy(st);
+    st = nullptr;
+  }
 };
 
-namespace {
-
-enum { BK_HNUM = 0, BK_HUPD = 1, BK_WUPD = 2 };
-
-hipEvent_t br_event(nmfc_brunet* e) {
-  if (!e->pool.empty()) {
-    hipEvent_t v = e->pool.back();
-    e->pool.pop_back();
+hipEvent_t br_event(BrLane* L) {
+  if (!L->pool.empty()) {
+    hipEvent_t v = L->pool.back();
+    L->pool.pop_back();
     return v;
   }
   hipEvent_t v = nullptr;
@@ -414,93 +521,113 @@ hipEvent_t br_event(nmfc_brunet* e) {
   return v;
 }
 
-void br_drain(nmfc_brunet* e) {
-  for (auto& p : e->pending) {
+void br_drain(BrLane* L) {
+  for (auto& p : L->pending) {
     float ms = 0.f;
-    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) e->kms[p.kid] += ms;
-    e->pool.push_back(p.a);
-    e->pool.push_back(p.b);
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) L->kms[p.kid] += ms;
+    L->pool.push_back(p.a);
+    L->pool.push_back(p.b);
   }
-  e->pending.clear();
+  L->pending.clear();
 }
 
 struct BTimed {
-  nmfc_brunet* e;
+  BrLane* L;
   int kid;
   hipEvent_t a = nullptr;
-  BTimed(nmfc_brunet* e_, int kid_, double flops) : e(e_), kid(kid_) {
-    e->kcount[kid] += 1;
-    e->kfl_sum[kid] += flops;
-    if (e->timing && (a = br_event(e))) (void)hipEventRecord(a, e->st);
+  BTimed(BrLane* L_, int kid_, double flops) : L(L_), kid(kid_) {
+    L->kcount[kid] += 1;
+    L->kfl_sum[kid] += flops;
+    if (L->timing && (a = br_event(L))) (void)hipEventRecord(a, L->st);
   }
   ~BTimed() {
-    if (e->timing && a) {
-      hipEvent_t b = br_event(e);
+    if (L->timing && a) {
+      hipEvent_t b = br_event(L);
       if (b) {
-        (void)hipEventRecord(b, e->st);
-        e->pending.push_back({kid, a, b});
+        (void)hipEventRecord(b, L->st);
+        L->pending.push_back({kid, a, b});
       }
     }
   }
 };
 
-// one k: B restarts (slots 0..B-1) already initialised in e->W / e->H; iterates to the stop rule.
+}  // namespace
+
+struct nmfc_brunet {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  int m = 0, n = 0;
+  long m_pad = 0, n_pad = 0;
+  int gc = 0, nchunks = 0;
+  int nlanes = BR_LANES;
+  Buf Acm, Arm, counts_tmp, cons_tmp;
+  BrLane lanes[BR_LANES];
+  bool timing = false;
+  double kms[3] = {0, 0, 0};
+  long long kcount[3] = {0, 0, 0};
+  double kfl_sum[3] = {0, 0, 0};
+};
+
+namespace {
+
+// one k: B restarts (slots 0..B-1) already initialised in L->W / L->H; iterates to the stop rule.
 template <int K>
-int br_iterate(nmfc_brunet* e, int B, const nmfc_brunet_opts& o, std::vector<int>& iters, std::vector<int>& stopped) {
+int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o, std::vector<int>& iters,
+               std::vector<int>& stopped) {
   constexpr int RG = rg_of(K);
   const int m = e->m, n = e->n;
-  hipStream_t st = e->st;
+  hipStream_t st = L->st;
   const long wstride = (long)m * K, hstride = (long)n * K;
   const long gp_cs = (long)B * K * e->n_pad;
   std::vector<int> act(B), si(B, 0);
   for (int b = 0; b < B; ++b) act[b] = b;
   int nact = B;
-  BCHECK(hipMemcpyAsync(e->act.p, act.data(), sizeof(int) * B, hipMemcpyHostToDevice, st));
-  BCHECK(hipMemsetAsync(e->memb.p, 0, sizeof(int) * (size_t)B * n, st));   // old.membership starts at 0
-  BCHECK(hipMemsetAsync(e->nochange.p, 0, sizeof(int) * B, st));
-  BCHECK(hipMemsetAsync(e->stop_iter.p, 0, sizeof(int) * B, st));
+  BCHECK(hipMemcpyAsync(L->act.p, act.data(), sizeof(int) * B, hipMemcpyHostToDevice, st));
+  BCHECK(hipMemsetAsync(L->memb.p, 0, sizeof(int) * (size_t)B * n, st));   // old.membership starts at 0
+  BCHECK(hipMemsetAsync(L->nochange.p, 0, sizeof(int) * B, st));
+  BCHECK(hipMemsetAsync(L->stop_iter.p, 0, sizeof(int) * B, st));
   const double fl = 4.0 * m * n * K;   // algorithmic flop per restart and kernel: VP (2mnk) + product (2mnk)
   for (int t = 1; t <= o.maxiter && nact > 0; ++t) {
     const int check = (t % o.stopfreq) == 0;
     const int groups = (nact + RG - 1) / RG;
     {
-      BTimed tl(e, BK_HNUM, fl * nact);
+      BTimed tl(L, BK_HNUM, fl * nact);
       hipLaunchKernelGGL((k_br_hnum<K, RG>), dim3((n + BT - 1) / BT, e->nchunks, groups), dim3(BT), 0, st,
-                         e->Arm.as<double>(), e->n_pad, m, n, e->gc, e->act.as<int>(), nact, e->W.as<double>(), wstride,
-                         e->H.as<double>(), hstride, e->Gp.as<double>(), gp_cs);
+                         e->Arm.as<double>(), e->n_pad, m, n, e->gc, L->act.as<int>(), nact, L->W.as<double>(), wstride,
+                         L->H.as<double>(), hstride, L->Gp.as<double>(), gp_cs);
     }
     {
-      BTimed tl(e, BK_HUPD, 0.0);
+      BTimed tl(L, BK_HUPD, 0.0);
       hipLaunchKernelGGL((k_br_hupd<K>), dim3(nact), dim3(BT), 0, st, t, check, o.stopconv, e->nchunks, m, n, e->n_pad,
-                         e->act.as<int>(), e->W.as<double>(), wstride, e->H.as<double>(), hstride, e->Gp.as<double>(),
-                         gp_cs, e->RS.as<double>(), e->memb.as<int>(), e->nochange.as<int>(), e->stop_iter.as<int>());
+                         L->act.as<int>(), L->W.as<double>(), wstride, L->H.as<double>(), hstride, L->Gp.as<double>(),
+                         gp_cs, L->RS.as<double>(), L->memb.as<int>(), L->nochange.as<int>(), L->stop_iter.as<int>());
     }
     {
-      BTimed tl(e, BK_WUPD, fl * nact);
+      BTimed tl(L, BK_WUPD, fl * nact);
       hipLaunchKernelGGL((k_br_wupd<K, RG>), dim3((m + BT - 1) / BT, groups), dim3(BT), 0, st, e->Acm.as<double>(),
-                         e->m_pad, m, n, e->act.as<int>(), nact, e->W.as<double>(), wstride, e->H.as<double>(), hstride,
-                         e->RS.as<double>());
+                         e->m_pad, m, n, L->act.as<int>(), nact, L->W.as<double>(), wstride, L->H.as<double>(), hstride,
+                         L->RS.as<double>());
     }
     BCHECK(hipGetLastError());
     if (check) {
       // stops happen only on check iterations, after that iteration's W update (NMF.div breaks at the
       // end of the iteration): drop stopped restarts from the launch list
-      BCHECK(hipMemcpyAsync(si.data(), e->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+      BCHECK(hipMemcpyAsync(si.data(), L->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
       BCHECK(hipStreamSynchronize(st));
-      if (e->timing) br_drain(e);
+      if (L->timing) br_drain(L);
       int q = 0;
       for (int x = 0; x < nact; ++x)
         if (si[act[x]] == 0) act[q++] = act[x];
       if (q != nact) {
         nact = q;
-        if (nact > 0) BCHECK(hipMemcpyAsync(e->act.p, act.data(), sizeof(int) * nact, hipMemcpyHostToDevice, st));
+        if (nact > 0) BCHECK(hipMemcpyAsync(L->act.p, act.data(), sizeof(int) * nact, hipMemcpyHostToDevice, st));
         BCHECK(hipStreamSynchronize(st));
       }
     }
   }
-  BCHECK(hipMemcpyAsync(si.data(), e->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+  BCHECK(hipMemcpyAsync(si.data(), L->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
   BCHECK(hipStreamSynchronize(st));
-  if (e->timing) br_drain(e);
+  if (L->timing) br_drain(L);
   iters.resize(B);
   stopped.resize(B);
   for (int b = 0; b < B; ++b) {
@@ -510,11 +637,12 @@ int br_iterate(nmfc_brunet* e, int B, const nmfc_brunet_opts& o, std::vector<int
   return 0;
 }
 
-int br_dispatch(nmfc_brunet* e, int K, int B, const nmfc_brunet_opts& o, std::vector<int>& iters, std::vector<int>& stopped) {
+int br_dispatch(const nmfc_brunet* e, BrLane* L, int K, int B, const nmfc_brunet_opts& o, std::vector<int>& iters,
+                std::vector<int>& stopped) {
   switch (K) {
 #define BR_CASE(KK) \
   case KK:          \
-    return br_iterate<KK>(e, B, o, iters, stopped);
+    return br_iterate<KK>(e, L, B, o, iters, stopped);
     BR_CASE(2) BR_CASE(3) BR_CASE(4) BR_CASE(5) BR_CASE(6) BR_CASE(7) BR_CASE(8) BR_CASE(9) BR_CASE(10) BR_CASE(11)
     BR_CASE(12) BR_CASE(13) BR_CASE(14) BR_CASE(15) BR_CASE(16)
 #undef BR_CASE
@@ -522,6 +650,81 @@ int br_dispatch(nmfc_brunet* e, int K, int B, const nmfc_brunet_opts& o, std::ve
       br_err("nmfc_brunet_run: k=%d unsupported", K);
       return -1;
   }
+}
+
+// Everything for one k on one lane: init, iterations, labels, counts slice, host outputs.
+struct KJob {
+  int ki, K;
+  long woff, hoff;   // offsets of this k's jobs in the W / H outputs
+};
+
+int br_run_k(nmfc_brunet* e, BrLane* L, const KJob& kj, int B, int R, const nmfc_brunet_opts& o, const double* W_init,
+             const double* H_init, int32_t* dcounts, nmfc_result* out, long long* tot_iters, int* max_it) {
+  const int m = e->m, n = e->n, K = kj.K, ki = kj.ki;
+  BCHECK(hipSetDevice(e->dev));
+  if (!L->st) BCHECK(hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking));
+  hipStream_t st = L->st;
+  if (L->W.ensure(sizeof(double) * (size_t)B * m * K) || L->H.ensure(sizeof(double) * (size_t)B * n * K) ||
+      L->Gp.ensure(sizeof(double) * (size_t)e->nchunks * B * K * e->n_pad) ||
+      L->RS.ensure(sizeof(double) * (size_t)B * K) || L->memb.ensure(sizeof(int) * (size_t)B * n) ||
+      L->nochange.ensure(sizeof(int) * B) || L->stop_iter.ensure(sizeof(int) * B) || L->act.ensure(sizeof(int) * B) ||
+      L->seeds.ensure(sizeof(uint32_t) * B) || L->labels.ensure(sizeof(int32_t) * (size_t)B * n))
+    return -1;
+  const long wstride = (long)m * K, hstride = (long)n * K;
+  std::vector<double> hw, hh;
+  std::vector<uint32_t> seeds(B);
+  const int rb = std::max(0, o.restart_begin);
+  for (int b = 0; b < B; ++b) seeds[b] = o.seed + (uint32_t)(rb + b + 1);   // set.seed(rseed + i), i 1-based
+  BCHECK(hipMemcpyAsync(L->seeds.p, seeds.data(), sizeof(uint32_t) * B, hipMemcpyHostToDevice, st));
+  if (W_init && H_init) {
+    // caller factors for this k's B jobs: W_b m x K column-major, H_b K x n column-major
+    hw.assign((size_t)B * m * K, 0.0);
+    for (int b = 0; b < B; ++b)
+      for (int c = 0; c < K; ++c)
+        for (int i = 0; i < m; ++i)
+          hw[(size_t)b * wstride + (size_t)i * K + c] = W_init[kj.woff + (long)b * wstride + (long)c * m + i];
+    BCHECK(hipMemcpyAsync(L->W.p, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st));
+    BCHECK(hipMemcpyAsync(L->H.p, H_init + kj.hoff, sizeof(double) * (size_t)B * hstride, hipMemcpyHostToDevice, st));
+  } else {
+    hipLaunchKernelGGL(k_br_init, dim3(B), dim3(BT), 0, st, L->seeds.as<uint32_t>(), m, n, K, L->W.as<double>(), wstride,
+                       L->H.as<double>(), hstride);
+    BCHECK(hipGetLastError());
+  }
+  BCHECK(hipStreamSynchronize(st));   // seeds / hw host buffers
+  std::vector<int> iters, stopped;
+  if (br_dispatch(e, L, K, B, o, iters, stopped)) return -1;
+  hipLaunchKernelGGL(k_br_labels, dim3((n + BT - 1) / BT, B), dim3(BT), 0, st, L->H.as<double>(), hstride, K, n,
+                     L->labels.as<int32_t>());
+  BCHECK(hipGetLastError());
+  if (dcounts) {
+    hipLaunchKernelGGL(k_br_counts, dim3((n + 15) / 16, (n + 15) / 16), dim3(BT), 0, st, L->labels.as<int32_t>(), B, n,
+                       dcounts + (size_t)n * n * ki);
+    BCHECK(hipGetLastError());
+  }
+  if (out && out->labels)
+    BCHECK(hipMemcpyAsync(out->labels + (size_t)ki * B * n, L->labels.p, sizeof(int32_t) * (size_t)B * n,
+                          hipMemcpyDeviceToHost, st));
+  if (out && (out->W || out->H)) {
+    hw.resize((size_t)B * wstride);
+    hh.resize((size_t)B * hstride);
+    BCHECK(hipMemcpyAsync(hw.data(), L->W.p, sizeof(double) * hw.size(), hipMemcpyDeviceToHost, st));
+    BCHECK(hipMemcpyAsync(hh.data(), L->H.p, sizeof(double) * hh.size(), hipMemcpyDeviceToHost, st));
+    BCHECK(hipStreamSynchronize(st));
+    if (out->W)
+      for (int b = 0; b < B; ++b)
+        for (int c = 0; c < K; ++c)
+          for (int i = 0; i < m; ++i)
+            out->W[kj.woff + (long)b * wstride + (long)c * m + i] = hw[(size_t)b * wstride + (size_t)i * K + c];
+    if (out->H) memcpy(out->H + kj.hoff, hh.data(), sizeof(double) * hh.size());
+  }
+  BCHECK(hipStreamSynchronize(st));
+  for (int b = 0; b < B; ++b) {
+    *tot_iters += iters[b];
+    *max_it = std::max(*max_it, iters[b]);
+    if (out && out->iters) out->iters[(size_t)ki * B + b] = iters[b];
+    if (out && out->stopped_early) out->stopped_early[(size_t)ki * B + b] = stopped[b];
+  }
+  return 0;
 }
 
 }  // namespace
@@ -554,12 +757,13 @@ nmfc_brunet* nmfc_brunet_create(int device, const double* A, int m, int n, int a
   if (device >= 0 && (err = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", err);
   if ((err = hipGetDevice(&e->dev)) != hipSuccess) return fail("hipGetDevice", err);
   if ((err = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", err);
+  if (const char* s = getenv("NMFC_BRUNET_LANES")) e->nlanes = std::max(1, std::min(BR_LANES, atoi(s)));
   e->m = m;
   e->n = n;
   e->m_pad = rup(m, BT);
   e->n_pad = rup(n, BT);
-  // fixed gene chunks (a function of m only): about 16 chunks of whole wavefronts, at most 2048 genes
-  e->gc = (int)std::min<long>(2048, std::max<long>(64, rup((m + 15) / 16, 64)));
+  // fixed gene chunks (a function of m only): about 16 chunks of whole LDS tiles, at most 2048 genes
+  e->gc = (int)std::min<long>(2048, std::max<long>(TL, rup((m + 15) / 16, TL)));
   e->nchunks = (m + e->gc - 1) / e->gc;
   if (e->Acm.ensure(sizeof(double) * e->m_pad * n) || e->Arm.ensure(sizeof(double) * (size_t)m * e->n_pad)) {
     nmfc_brunet_destroy(e);
@@ -589,10 +793,12 @@ nmfc_brunet* nmfc_brunet_create(int device, const double* A, int m, int n, int a
 void nmfc_brunet_destroy(nmfc_brunet* e) {
   if (!e) return;
   if (e->st) (void)hipStreamSynchronize(e->st);
-  br_drain(e);
-  for (auto v : e->pool) (void)hipEventDestroy(v);
-  Buf* bufs[] = {&e->Acm, &e->Arm,      &e->W,         &e->H,   &e->Gp,    &e->RS,     &e->memb,
-                 &e->nochange, &e->stop_iter, &e->act, &e->seeds, &e->labels, &e->counts_tmp, &e->cons_tmp};
+  for (BrLane& L : e->lanes) {
+    if (L.st) (void)hipStreamSynchronize(L.st);
+    br_drain(&L);
+    L.release();
+  }
+  Buf* bufs[] = {&e->Acm, &e->Arm, &e->counts_tmp, &e->cons_tmp};
   for (Buf* b : bufs) b->release();
   if (e->st) (void)hipStreamDestroy(e->st);
   delete e;
@@ -636,22 +842,10 @@ int nmfc_brunet_run(nmfc_brunet* e, const int* ks, int nk, int R, const nmfc_bru
     br_err("nmfc_brunet_run: empty restart range [%d, %d)", rb, re);
     return -1;
   }
+  o.restart_begin = rb;
   const int B = re - rb;
   BCHECK(hipSetDevice(e->dev));
   auto t0 = std::chrono::steady_clock::now();
-  for (int q = 0; q < 3; ++q) e->kms[q] = 0, e->kcount[q] = 0, e->kfl_sum[q] = 0;
-  int kmax = 0;
-  for (int q = 0; q < nk; ++q) kmax = std::max(kmax, ks[q]);
-  if (e->W.ensure(sizeof(double) * (size_t)B * m * kmax) || e->H.ensure(sizeof(double) * (size_t)B * n * kmax) ||
-      e->Gp.ensure(sizeof(double) * (size_t)e->nchunks * B * kmax * e->n_pad) ||
-      e->RS.ensure(sizeof(double) * (size_t)B * kmax) || e->memb.ensure(sizeof(int) * (size_t)B * n) ||
-      e->nochange.ensure(sizeof(int) * B) || e->stop_iter.ensure(sizeof(int) * B) || e->act.ensure(sizeof(int) * B) ||
-      e->seeds.ensure(sizeof(uint32_t) * B) || e->labels.ensure(sizeof(int32_t) * (size_t)B * n))
-    return -1;
-  hipStream_t st = e->st;
-  std::vector<uint32_t> seeds(B);
-  for (int b = 0; b < B; ++b) seeds[b] = o.seed + (uint32_t)(rb + b + 1);   // set.seed(rseed + i), i 1-based
-  BCHECK(hipMemcpyAsync(e->seeds.p, seeds.data(), sizeof(uint32_t) * B, hipMemcpyHostToDevice, st));
   int32_t* dcounts = nullptr;
   const size_t nn = (size_t)n * n;
   if (out && (out->counts || out->consensus)) {
@@ -662,65 +856,61 @@ int nmfc_brunet_run(nmfc_brunet* e, const int* ks, int nk, int R, const nmfc_bru
       dcounts = e->counts_tmp.as<int32_t>();
     }
   }
+  // jobs: output offsets in nmfconsensus order; executed largest k first
+  std::vector<KJob> jobs(nk);
+  long woff = 0, hoff = 0;
+  for (int ki = 0; ki < nk; ++ki) {
+    jobs[ki] = {ki, ks[ki], woff, hoff};
+    woff += (long)B * m * ks[ki];
+    hoff += (long)B * n * ks[ki];
+  }
+  std::vector<KJob> order(jobs);
+  std::stable_sort(order.begin(), order.end(), [](const KJob& a, const KJob& b) { return a.K > b.K; });
+  const int nl = std::min(o.lanes > 0 ? std::min(o.lanes, BR_LANES) : e->nlanes, nk);
+  std::atomic<int> next{0};
+  std::atomic<int> failed{0};
+  std::string first_err;
+  std::mutex mu;
+  std::vector<long long> lane_iters(nl, 0);
+  std::vector<int> lane_max(nl, 0);
+  for (int l = 0; l < nl; ++l) {
+    BrLane& L = e->lanes[l];
+    L.timing = e->timing;
+    for (int q = 0; q < 3; ++q) L.kms[q] = 0, L.kcount[q] = 0, L.kfl_sum[q] = 0;
+  }
+  auto worker = [&](int l) {
+    BrLane* L = &e->lanes[l];
+    for (;;) {
+      const int idx = next.fetch_add(1);
+      if (idx >= nk || failed.load()) break;
+      if (br_run_k(e, L, order[idx], B, R, o, W_init, H_init, dcounts, out, &lane_iters[l], &lane_max[l])) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!failed.exchange(1)) first_err = nmfc_last_error();
+        break;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int l = 1; l < nl; ++l) th.emplace_back(worker, l);
+  worker(0);
+  for (auto& t : th) t.join();
+  if (failed.load()) {
+    nmfc_set_error(first_err.c_str());
+    return -1;
+  }
   long long tot_iters = 0;
   int max_it = 0;
-  double t_iter = 0.0;
-  long woff = 0, hoff = 0;
-  std::vector<double> hw, hh;
-  for (int ki = 0; ki < nk; ++ki) {
-    const int K = ks[ki];
-    const long wstride = (long)m * K, hstride = (long)n * K;
-    if (W_init && H_init) {
-      // caller factors for this k's B jobs: W_b m x K column-major, H_b K x n column-major
-      hw.assign((size_t)B * m * K, 0.0);
-      for (int b = 0; b < B; ++b)
-        for (int c = 0; c < K; ++c)
-          for (int i = 0; i < m; ++i) hw[(size_t)b * wstride + (size_t)i * K + c] = W_init[woff + (long)b * wstride + (long)c * m + i];
-      BCHECK(hipMemcpyAsync(e->W.p, hw.data(), sizeof(double) * hw.size(), hipMemcpyHostToDevice, st));
-      BCHECK(hipMemcpyAsync(e->H.p, H_init + hoff, sizeof(double) * (size_t)B * hstride, hipMemcpyHostToDevice, st));
-      BCHECK(hipStreamSynchronize(st));
-    } else {
-      hipLaunchKernelGGL(k_br_init, dim3(B), dim3(BT), 0, st, e->seeds.as<uint32_t>(), m, n, K, e->W.as<double>(), wstride,
-                         e->H.as<double>(), hstride);
-      BCHECK(hipGetLastError());
+  for (int q = 0; q < 3; ++q) e->kms[q] = 0, e->kcount[q] = 0, e->kfl_sum[q] = 0;
+  for (int l = 0; l < nl; ++l) {
+    tot_iters += lane_iters[l];
+    max_it = std::max(max_it, lane_max[l]);
+    for (int q = 0; q < 3; ++q) {
+      e->kms[q] += e->lanes[l].kms[q];
+      e->kcount[q] += e->lanes[l].kcount[q];
+      e->kfl_sum[q] += e->lanes[l].kfl_sum[q];
     }
-    std::vector<int> iters, stopped;
-    auto ti0 = std::chrono::steady_clock::now();
-    if (br_dispatch(e, K, B, o, iters, stopped)) return -1;
-    t_iter += std::chrono::duration<double>(std::chrono::steady_clock::now() - ti0).count();
-    hipLaunchKernelGGL(k_br_labels, dim3((n + BT - 1) / BT, B), dim3(BT), 0, st, e->H.as<double>(), hstride, K, n,
-                       e->labels.as<int32_t>());
-    BCHECK(hipGetLastError());
-    if (dcounts) {
-      hipLaunchKernelGGL(k_br_counts, dim3((n + 15) / 16, (n + 15) / 16), dim3(BT), 0, st, e->labels.as<int32_t>(), B, n,
-                         dcounts + nn * ki);
-      BCHECK(hipGetLastError());
-    }
-    if (out && out->labels)
-      BCHECK(hipMemcpyAsync(out->labels + (size_t)ki * B * n, e->labels.p, sizeof(int32_t) * (size_t)B * n,
-                            hipMemcpyDeviceToHost, st));
-    if (out && (out->W || out->H)) {
-      hw.resize((size_t)B * wstride);
-      hh.resize((size_t)B * hstride);
-      BCHECK(hipMemcpyAsync(hw.data(), e->W.p, sizeof(double) * hw.size(), hipMemcpyDeviceToHost, st));
-      BCHECK(hipMemcpyAsync(hh.data(), e->H.p, sizeof(double) * hh.size(), hipMemcpyDeviceToHost, st));
-      BCHECK(hipStreamSynchronize(st));
-      if (out->W)
-        for (int b = 0; b < B; ++b)
-          for (int c = 0; c < K; ++c)
-            for (int i = 0; i < m; ++i) out->W[woff + (long)b * wstride + (long)c * m + i] = hw[(size_t)b * wstride + (size_t)i * K + c];
-      if (out->H) memcpy(out->H + hoff, hh.data(), sizeof(double) * hh.size());
-    }
-    BCHECK(hipStreamSynchronize(st));
-    for (int b = 0; b < B; ++b) {
-      tot_iters += iters[b];
-      max_it = std::max(max_it, iters[b]);
-      if (out && out->iters) out->iters[(size_t)ki * B + b] = iters[b];
-      if (out && out->stopped_early) out->stopped_early[(size_t)ki * B + b] = stopped[b];
-    }
-    woff += (long)B * wstride;
-    hoff += (long)B * hstride;
   }
+  hipStream_t st = e->st;
   if (out && dcounts) {
     if (out->consensus) {
       if (e->cons_tmp.ensure(sizeof(double) * nn * nk)) return -1;
@@ -733,16 +923,15 @@ int nmfc_brunet_run(nmfc_brunet* e, const int* ks, int nk, int R, const nmfc_bru
       BCHECK(hipMemcpyAsync(out->counts, dcounts, sizeof(int32_t) * nn * nk, hipMemcpyDeviceToHost, st));
   }
   BCHECK(hipStreamSynchronize(st));
-  if (e->timing) br_drain(e);
   auto t1 = std::chrono::steady_clock::now();
   if (out) {
     out->seconds_total = std::chrono::duration<double>(t1 - t0).count();
-    out->seconds_iterate = t_iter;
+    out->seconds_iterate = out->seconds_total;
     out->restart_iterations = tot_iters;
     out->max_iter_run = max_it;
   }
   if (o.verbose)
-    fprintf(stderr, "[nmfc brunet] %d restarts x %d k, mean iters %.1f, max %d, %.3f s\n", B, nk,
+    fprintf(stderr, "[nmfc brunet] %d restarts x %d k on %d lanes, mean iters %.1f, max %d, %.3f s\n", B, nk, nl,
             (double)tot_iters / ((double)B * nk), max_it, std::chrono::duration<double>(t1 - t0).count());
   return 0;
 }
