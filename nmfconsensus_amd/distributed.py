@@ -61,3 +61,37 @@ def run_sharded_with(runner, ks, R: int, n: int, *, rank: int, world: int, group
     if world > 1:
         allreduce_counts(t, group)
     return t.numpy()
+
+
+# ------------------------------------------------------------------------------------------------
+# Brunet KL-divergence sweep (nmfc_brunet_*): jobs run k-major (for k: for restart i), so ranks take a
+# contiguous range of RESTARTS for every k -- every rank gets the same mix of k, i.e. equal work.
+# ------------------------------------------------------------------------------------------------
+def run_sharded_brunet(engine, ks, R: int, *, rank: int, world: int, counts_tensor=None, group=None,
+                       reduce: bool = True, **run_kwargs):
+    """Runs this rank's restart shard on `engine` (nmfconsensus_amd.brunet.BrunetEngine) and
+    all-reduces the int32 counts (RCCL on GPUs).  Returns (counts_tensor, local SweepResult)."""
+    import torch
+
+    nk = len(ks)
+    n = engine.n
+    rb, re = shard_range(R, rank, world)
+    if counts_tensor is None:
+        counts_tensor = torch.zeros((nk, n, n), dtype=torch.int32, device="cuda")
+    res = engine.run(ks, R, restart_begin=rb, restart_end=re, counts_device_ptr=counts_tensor.data_ptr(), **run_kwargs)
+    if world > 1 and reduce:
+        allreduce_counts(counts_tensor, group)
+    return counts_tensor, res
+
+
+def run_sharded_restarts_with(runner, ks, R: int, n: int, *, rank: int, world: int, group=None):
+    """Host-side form of run_sharded_brunet for the CPU (gloo) tests: `runner(restart_begin,
+    restart_end)` returns this shard's (nk, n, n) int32 counts."""
+    import torch
+
+    rb, re = shard_range(R, rank, world)
+    local = np.ascontiguousarray(runner(rb, re), dtype=np.int32).reshape(len(ks), n, n)
+    t = torch.from_numpy(local.copy())
+    if world > 1:
+        allreduce_counts(t, group)
+    return t.numpy()

@@ -77,3 +77,53 @@ def test_gloo_world2_counts_equal_golden(golden):
         assert p.exitcode == 0
     for i, k in enumerate(golden["c1_ks"]):
         assert np.array_equal(out[i], golden[f"c1_counts_argmax_k{k}"])
+
+
+def _brunet_worker(rank, world, port, ret):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as dist
+    from nmfconsensus_amd.distributed import run_sharded_restarts_with
+    from pyoracle import Oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    z = np.load(os.path.join(ROOT, "tests", "golden", "golden.npz"), allow_pickle=False)
+    A = np.asfortranarray(z["A_gct"][:300])
+    ks, R = [2, 3], 5
+    O = Oracle()
+
+    def runner(rb, re):
+        counts = np.zeros((len(ks), A.shape[1], A.shape[1]), dtype=np.int32)
+        for ki, k in enumerate(ks):
+            for i in range(rb, re):
+                W0, H0 = O.brunet_init(123456789 + i + 1, A.shape[0], A.shape[1], k)
+                _, H, _ = O.brunet(A, W0, H0, 600)
+                l = O.labels(H, 0)
+                counts[ki] += (l[:, None] == l[None, :]).astype(np.int32)
+        return counts
+
+    out = run_sharded_restarts_with(runner, ks, R, A.shape[1], rank=rank, world=world)
+    if rank == 0:
+        ret.put((out, runner(0, R)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_brunet_restart_shards():
+    """Brunet sweep sharded by restart range over 2 gloo ranks == the single-process counts."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_brunet_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out, ref = q.get(timeout=280)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(out, ref)
+    assert out[0].diagonal().tolist() == [5] * out.shape[1]
