@@ -22,7 +22,11 @@ extern "C" {
 enum {
   NMFC_STOP_FIXED = 0,          /* run exactly maxiter iterations */
   NMFC_STOP_REF_COMPAT = 1,     /* nmf_mu.c:253-282 as the reference executes it (zero-padded h0) */
-  NMFC_STOP_ARGMAX_STABLE = 2   /* same counter, per-sample argmax class (the check's intent) */
+  NMFC_STOP_ARGMAX_STABLE = 2,  /* same counter, per-sample argmax class (the check's intent) */
+  NMFC_STOP_TOLX = 3            /* libnmf's TolX/TolFun convergence test (nmf_als.c:304-349 pattern, applied
+                                   to the MU update): on even iterations > 1 stop when
+                                   max(calculateMaxchange(W), calculateMaxchange(H)) < TolX, or when
+                                   TolFun >= 1 (dnorm <= TolFun * dnorm0 with dnorm0 == dnorm, :330/:345) */
 };
 
 /* Label rules for the consensus (nmf.r:128). */
@@ -42,6 +46,8 @@ typedef struct nmfc_sweep_opts {
   int job_end;
   int check_every;    /* host polls the stopped-restart count every this many iterations (default 16) */
   int verbose;        /* 0 quiet; 1 per-sweep summary on stderr */
+  double TolX;        /* NMFC_STOP_TOLX threshold (options_t.TolX, default 1e-4, setdefaultopts.c) */
+  double TolFun;      /* NMFC_STOP_TOLX TolFun (default 1e-4) */
 } nmfc_sweep_opts;
 
 /* Outputs.  Every pointer may be NULL.  Host memory unless *_on_device is set.

@@ -15,7 +15,7 @@ _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)
 c_int = ctypes.c_int
 
-STOP_FIXED, STOP_REF_COMPAT, STOP_ARGMAX_STABLE = 0, 1, 2
+STOP_FIXED, STOP_REF_COMPAT, STOP_ARGMAX_STABLE, STOP_TOLX = 0, 1, 2, 3
 LABEL_ARGMAX, LABEL_R_ORDER = 0, 1
 KID_WTA, KID_HUPD, KID_AHTW, KID_INIT, KID_LABEL = 0, 1, 2, 3, 4
 
@@ -23,7 +23,7 @@ KID_WTA, KID_HUPD, KID_AHTW, KID_INIT, KID_LABEL = 0, 1, 2, 3, 4
 class SweepOpts(ctypes.Structure):
     _fields_ = [("maxiter", c_int), ("stop_rule", c_int), ("label_rule", c_int), ("seed", ctypes.c_uint32),
                 ("min_init", c_int), ("max_init", c_int), ("job_begin", c_int), ("job_end", c_int),
-                ("check_every", c_int), ("verbose", c_int)]
+                ("check_every", c_int), ("verbose", c_int), ("TolX", ctypes.c_double), ("TolFun", ctypes.c_double)]
 
 
 class Result(ctypes.Structure):

@@ -183,7 +183,7 @@ struct nmfc_engine {
   DevBuf Acm, Arm;
   // per-run buffers (grow-only)
   DevBuf W[2], H[2], Gpart, SWpart, SH, SHP, colact, Hfin, Wfin;
-  DevBuf rinfo, stop_iter, stop_reason, unchanged, classes, n_stopped;
+  DevBuf rinfo, stop_iter, stop_reason, unchanged, classes, n_stopped, Hstat, Wsnap;
   DevBuf prb, pre, colinfo, moves, finfo;
   DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp;
   int jump_chunks = 0;
@@ -271,6 +271,8 @@ void nmfc_default_opts(nmfc_sweep_opts* o) {
   o->job_end = -1;
   o->check_every = 16;
   o->verbose = 0;
+  o->TolX = 1.0E-04;                  // setdefaultopts.c (options_t.TolX / TolFun)
+  o->TolFun = 1.0E-04;
 }
 
 nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a_on_device) {
@@ -349,7 +351,7 @@ void nmfc_engine_destroy(nmfc_engine* e) {
                     &e->stop_iter, &e->stop_reason, &e->unchanged, &e->classes, &e->n_stopped, &e->prb,
                     &e->pre,       &e->colinfo,   &e->moves,     &e->finfo,     &e->initjobs, &e->chunk_job,  &e->chunk_idx,
                     &e->jump,      &e->labels,    &e->slot,      &e->grp_begin, &e->grp_list,  &e->counts_tmp,
-                    &e->cons_tmp};
+                    &e->cons_tmp,  &e->Hstat,     &e->Wsnap};
   for (DevBuf* b : bufs) b->release();
   if (e->h_stopped) (void)hipHostFree(e->h_stopped);
   if (e->st) (void)hipStreamDestroy(e->st);
@@ -395,7 +397,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     set_err("nmfc_engine_run: maxiter must be >= 0");
     return -1;
   }
-  if (opts.stop_rule < 0 || opts.stop_rule > 2 || opts.label_rule < 0 || opts.label_rule > 1) {
+  if (opts.stop_rule < 0 || opts.stop_rule > 3 || opts.label_rule < 0 || opts.label_rule > 1) {
     set_err("nmfc_engine_run: bad stop or label rule");
     return -1;
   }
@@ -457,8 +459,10 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       e->prb.ensure(sizeof(int) * pk.npanels) || e->pre.ensure(sizeof(int) * pk.npanels) ||
       e->colinfo.ensure(sizeof(ColInfo) * pk.npanels * PANEL) ||
       e->moves.ensure(sizeof(MoveJob) * nj) || e->labels.ensure(sizeof(int32_t) * (size_t)nj * n) ||
-      e->slot.ensure(sizeof(int) * nj))
+      e->slot.ensure(sizeof(int) * nj) || e->Hstat.ensure(sizeof(double) * nj))
     return -1;
+  const bool tolx = opts.stop_rule == NMFC_STOP_TOLX;
+  if (tolx && e->Wsnap.ensure(sizeof(double) * cap_cols * e->m_pad)) return -1;
   hipStream_t st = e->st;
   int cur = 0;
   auto upload_packing = [&](const Packing& p) -> int {
@@ -625,8 +629,13 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                              e->SWpart.as<double>(), sw_total, e->H[cur].as<double>(), e->SH.as<double>(),
                              e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->unchanged.as<int>(),
                              e->classes.as<int>(), cls_ld, e->n_stopped.as<int>(), e->SHP.as<double>(),
-                             e->colact.as<int>());
+                             e->colact.as<int>(), e->Hstat.as<double>());
         }
+        // STOP_TOLX (even iterations > 1): snapshot W before its update, test after it
+        const bool tol_check = tolx && iter > 1 && iter % 2 == 0;
+        if (tol_check)
+          HCHECK(hipMemcpyAsync(e->Wsnap.p, e->W[cur].p, sizeof(double) * (size_t)pk.npanels * PANEL * e->m_pad,
+                                hipMemcpyDeviceToDevice, st));
         {
           TimedLaunch tl(e, KID_AHTW);
           auto ka = ahtw_small ? k_ahtw4<0, GT / 2> : k_ahtw4<0, GT>;
@@ -634,6 +643,13 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                              e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
                              e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), pk.npanels,
                              ngt_ahtw);
+        }
+        if (tol_check) {
+          TimedLaunch tl(e, KID_OTHER);
+          hipLaunchKernelGGL(k_wstat, dim3(nact), dim3(NT), 0, st, iter, e->rinfo.as<RestartInfo>(),
+                             e->W[cur].as<double>(), e->Wsnap.as<double>(), e->m_pad, m, e->colact.as<int>(),
+                             e->Hstat.as<double>(), opts.TolX, opts.TolFun, e->stop_iter.as<int>(),
+                             e->stop_reason.as<int>(), e->n_stopped.as<int>());
         }
       }
       HCHECK(hipGetLastError());
@@ -768,7 +784,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     fl_wta += (double)itr * (2.0 * m * n * k + 2.0 * m * k * k);
     fl_ahtw += (double)itr * (2.0 * m * n * k + 2.0 * m * k * k);
     if (out && out->iters) out->iters[rslot[rid]] = itr;
-    if (out && out->stopped_early) out->stopped_early[rslot[rid]] = (sr[rid] == 1);
+    if (out && out->stopped_early) out->stopped_early[rslot[rid]] = (sr[rid] == 1 || sr[rid] == 3);
   }
   if (e->kcount[KID_WTA]) e->kflops[KID_WTA] = fl_wta / e->kcount[KID_WTA];
   if (e->kcount[KID_AHTW]) e->kflops[KID_AHTW] = fl_ahtw / e->kcount[KID_AHTW];

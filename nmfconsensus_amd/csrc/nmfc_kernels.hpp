@@ -27,7 +27,8 @@ constexpr int NT = 256;            // threads per workgroup
 constexpr int HCH = 256;           // sample chunk of the H-update kernel
 constexpr int KMAX = 16;           // largest rank k
 constexpr int GT = 128;            // genes per A h^T tile (and per Gram partial)
-constexpr int STOP_FIXED = 0, STOP_REF_COMPAT = 1, STOP_ARGMAX_STABLE = 2;
+constexpr int STOP_FIXED = 0, STOP_REF_COMPAT = 1, STOP_ARGMAX_STABLE = 2, STOP_TOLX = 3;
+constexpr double SQRTEPS = 1.0536712127723509e-08;   // sqrt(dlamch('E')), nmf_als.c sqrteps
 constexpr double DIV_BY_ZERO_AVOIDANCE = 1E-09;   // nmf_mu.c:56
 
 // nmf_mu.c:184-191 / :209-216: h = (h0 == 0 || num == 0) ? 0 : h0 * (num / (den + 1e-9)); clamp < 0
@@ -742,6 +743,7 @@ struct HupdSmem {
   double win[KMAX * KMAX];
   double shp[NT];
   int changed;
+  unsigned long long dmax, omax;   // STOP_TOLX: max |h0 - h| and max |h0| (non-negative doubles as bits)
 };
 
 // The body for rank K (compile time): every per-sample loop over the k factors is unrolled, so the
@@ -754,7 +756,7 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
                                              int* __restrict__ stop_iter, int* __restrict__ stop_reason,
                                              int* __restrict__ unchanged, int* __restrict__ classes, long cls_ld,
                                              int* __restrict__ n_stopped, double* __restrict__ SHP,
-                                             int* __restrict__ colact, HupdSmem& sm) {
+                                             int* __restrict__ colact, double* __restrict__ Hstat, HupdSmem& sm) {
   double* sw = sm.sw;
   double* Hn = sm.Hn;
   double* win = sm.win;
@@ -765,7 +767,13 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
   constexpr int k = K;
   const int c0 = me.col0;
   const bool check = (stop_rule != STOP_FIXED) && iter > 1 && (iter % 2 == 0);
-  if (tid == 0) changed = 0;
+  const bool tolx = check && stop_rule == STOP_TOLX;
+  double tdm = 0.0, tom = 0.0;   // this thread's max |h0 - h| and max |h0| (STOP_TOLX)
+  if (tid == 0) {
+    changed = 0;
+    sm.dmax = 0ull;
+    sm.omax = 0ull;
+  }
   for (int idx = tid; idx < k * k; idx += NT) {
     const double* src = SWpart + me.sq_off + idx;
     double sacc = 0.0;
@@ -840,6 +848,10 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
         for (int bb = 0; bb < K; ++bb) d = fma(sw[a * KMAX + bb], hc[bb], d);
         hn = mu_rule(hc[a], gs[a], d);
         H[(long)(c0 + a) * n_pad + j] = hn;
+        if (tolx) {   // calculateMaxchange(h, h0) (calculatemaxchange.c:55-60): dlange('M') of h0 and h0 - h
+          tdm = fmax(tdm, fabs(hc[a] - hn));
+          tom = fmax(tom, fabs(hc[a]));
+        }
         if (stop_rule == STOP_REF_COMPAT) {
           // flat column-major index of (a, j) in the k x n buffer; window i reads [i*n, i*n + k)
           const long tf = (long)j * k + a;
@@ -873,7 +885,13 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
     __syncthreads();
   }
   shp[tid] = shacc;
+  if (tolx) {
+    atomicMax(&sm.dmax, (unsigned long long)__double_as_longlong(tdm));
+    atomicMax(&sm.omax, (unsigned long long)__double_as_longlong(tom));
+  }
   __syncthreads();
+  if (tolx && tid == 0)
+    Hstat[rid] = __longlong_as_double((long long)sm.dmax) / (SQRTEPS + __longlong_as_double((long long)sm.omax));
   if (pid < npairs && pq == 0) {
     double s = shp[tid];
     for (int q = 1; q < T; ++q) s += shp[tid + q];
@@ -901,7 +919,7 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
   __syncthreads();
   if (tid == 0) {
     int reason = 0;
-    if (check) {
+    if (check && stop_rule != STOP_TOLX) {   // the TolX test runs after the W update (k_wstat)
       if (!changed) {
         const int u = unchanged[rid] + 1;
         unchanged[rid] = u;
@@ -927,14 +945,15 @@ static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, in
                                                        int* __restrict__ stop_iter, int* __restrict__ stop_reason,
                                                        int* __restrict__ unchanged, int* __restrict__ classes,
                                                        long cls_ld, int* __restrict__ n_stopped,
-                                                       double* __restrict__ SHP, int* __restrict__ colact) {
+                                                       double* __restrict__ SHP, int* __restrict__ colact,
+                                                       double* __restrict__ Hstat) {
   __shared__ HupdSmem sm;
   const RestartInfo me = ri[blockIdx.x];
   if (stop_iter[me.rid] != 0) return;
 #define NMFC_HUPD_CASE(KK)                                                                                      \
   case KK:                                                                                                     \
     hupdate_body<KK>(me, iter, maxiter, stop_rule, n, n_pad, Gpart, g_ld, g_split, nsplit, SWpart, sw_total, H, SH, \
-                     stop_iter, stop_reason, unchanged, classes, cls_ld, n_stopped, SHP, colact, sm);          \
+                     stop_iter, stop_reason, unchanged, classes, cls_ld, n_stopped, SHP, colact, Hstat, sm);   \
     break;
   switch (me.k) {
     NMFC_HUPD_CASE(2) NMFC_HUPD_CASE(3) NMFC_HUPD_CASE(4) NMFC_HUPD_CASE(5) NMFC_HUPD_CASE(6)
@@ -1456,6 +1475,52 @@ static __global__ __launch_bounds__(NT) void k_init(const InitJob* __restrict__ 
         }
       }
       ++t;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// STOP_TOLX, after the W update of an even iteration > 1 (nmf_als.c:304-349 applied to MU): one
+// workgroup per live restart: dw = calculateMaxchange(W, W0) from the pre-update snapshot W0,
+// delta = max(dh, dw) with dh from k_hupdate; stop if delta < TolX, or if TolFun >= 1 (the test
+// dnorm <= TolFun * dnorm0 runs after dnorm0 = dnorm, nmf_als.c:330/:345, so it only fires then --
+// or on an exactly-zero residual, which is not evaluated here).
+// ---------------------------------------------------------------------------------------------
+static __global__ __launch_bounds__(NT) void k_wstat(int iter, const RestartInfo* __restrict__ ri,
+                                                     const double* __restrict__ W, const double* __restrict__ W0,
+                                                     long m_pad, int m, const int* __restrict__ colact,
+                                                     const double* __restrict__ Hstat, double TolX, double TolFun,
+                                                     int* __restrict__ stop_iter, int* __restrict__ stop_reason,
+                                                     int* __restrict__ n_stopped) {
+  __shared__ unsigned long long dmax, omax;
+  const RestartInfo me = ri[blockIdx.x];
+  if (stop_iter[me.rid] != 0 || colact[me.col0] != iter) return;   // stopped, or no W update this iteration
+  if (threadIdx.x == 0) {
+    dmax = 0ull;
+    omax = 0ull;
+  }
+  __syncthreads();
+  double tdm = 0.0, tom = 0.0;
+  for (int a = 0; a < me.k; ++a) {
+    const double* w = W + (long)(me.col0 + a) * m_pad;
+    const double* w0 = W0 + (long)(me.col0 + a) * m_pad;
+    for (int i = threadIdx.x; i < m; i += NT) {
+      const double o = w0[i];
+      tdm = fmax(tdm, fabs(o - w[i]));
+      tom = fmax(tom, fabs(o));
+    }
+  }
+  atomicMax(&dmax, (unsigned long long)__double_as_longlong(tdm));
+  atomicMax(&omax, (unsigned long long)__double_as_longlong(tom));
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double dw = __longlong_as_double((long long)dmax) / (SQRTEPS + __longlong_as_double((long long)omax));
+    const double dh = Hstat[me.rid];
+    const double delta = dh > dw ? dh : dw;
+    if (delta < TolX || TolFun >= 1.0) {
+      stop_iter[me.rid] = iter;
+      stop_reason[me.rid] = 3;
+      atomicAdd(n_stopped, 1);
     }
   }
 }

@@ -28,13 +28,13 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import (LABEL_ARGMAX, LABEL_R_ORDER, STOP_ARGMAX_STABLE, STOP_FIXED, STOP_REF_COMPAT, Result,
+from ._lib import (LABEL_ARGMAX, LABEL_R_ORDER, STOP_ARGMAX_STABLE, STOP_FIXED, STOP_REF_COMPAT, STOP_TOLX, Result,
                    SweepOpts)
 
 __all__ = [
     "Engine", "SweepResult", "doNMF", "createJobArray", "runNMFinJobs", "computeConsensusMatrixFromClusterings",
     "computeConsensusAndSaveFiles", "cophenetic", "cutree", "job_grid",
-    "STOP_FIXED", "STOP_REF_COMPAT", "STOP_ARGMAX_STABLE", "LABEL_ARGMAX", "LABEL_R_ORDER",
+    "STOP_FIXED", "STOP_REF_COMPAT", "STOP_ARGMAX_STABLE", "STOP_TOLX", "LABEL_ARGMAX", "LABEL_R_ORDER",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -131,7 +131,8 @@ class Engine:
     def run(self, ks, R: int, *, maxiter: int = 10000, seed: int = 123, stop_rule: int = STOP_REF_COMPAT,
             label_rule: int = LABEL_ARGMAX, job_begin: int = 0, job_end: int = -1, W_init=None, H_init=None,
             want_factors: bool = False, want_counts: bool = True, counts_device_ptr: int | None = None,
-            check_every: int = 16, min_init: int = 0, max_init: int = 1, verbose: bool = False) -> SweepResult:
+            check_every: int = 16, min_init: int = 0, max_init: int = 1, verbose: bool = False,
+            TolX: float = 1e-4, TolFun: float = 1e-4) -> SweepResult:
         ks = [int(k) for k in ks]
         nk = len(ks)
         njobs_all = nk * R
@@ -146,6 +147,7 @@ class Engine:
         o.maxiter, o.stop_rule, o.label_rule, o.seed = maxiter, stop_rule, label_rule, seed & 0xFFFFFFFF
         o.job_begin, o.job_end, o.check_every, o.verbose = jb, je, check_every, 1 if verbose else 0
         o.min_init, o.max_init = min_init, max_init
+        o.TolX, o.TolFun = TolX, TolFun
         m, n = self.m, self.n
         res = Result()
         iters = np.zeros(nj, dtype=np.int32)

@@ -78,7 +78,7 @@ void orc_init_restart(uint32_t seed, int m, int n, int k, double* W, double* H) 
 /* ---------------------------------------------------------------------------------------
  * nmf_mu restatement (libnmf/nmf_mu.c:84-315)
  * --------------------------------------------------------------------------------------- */
-enum { ORC_STOP_FIXED = 0, ORC_STOP_REF_COMPAT = 1, ORC_STOP_ARGMAX_STABLE = 2 };
+enum { ORC_STOP_FIXED = 0, ORC_STOP_REF_COMPAT = 1, ORC_STOP_ARGMAX_STABLE = 2, ORC_STOP_TOLX = 3 };
 
 #define ORC_DIV_BY_ZERO_AVOIDANCE 1E-09 /* nmf_mu.c:56 */
 
@@ -258,4 +258,43 @@ double orc_calculate_maxchange(const double* mat, double* mat0, int m, int n, do
     if (v > mxd || isnan(v)) mxd = v;
   }
   return mxd / (sqrteps + mx0);
+}
+
+/*
+ * The MU update (nmf_mu.c:174-216) under libnmf's TolX/TolFun convergence test as nmf_als.c:304-349
+ * writes it: after each iteration dnorm = calculateNorm(A, W, H) (:304), dw / dh = calculateMaxchange
+ * of the new vs the previous factor (:310, :316), delta = max(dh, dw), dnorm0 = dnorm (:330); on even
+ * iterations > 1 stop if delta < TolX, else if dnorm <= TolFun * dnorm0 (:341-349).  Returns the
+ * iteration count.  sqrteps = sqrt(dlamch('E')) = 2^-26.5.
+ */
+int orc_nmf_mu_tol(const double* A, double* W, double* H, int m, int n, int k, int maxiter, double TolX,
+                   double TolFun) {
+  const double sqrteps = 1.0536712127723509e-08;
+  double* W0 = (double*)malloc(sizeof(double) * (size_t)m * k);
+  double* H0 = (double*)malloc(sizeof(double) * (size_t)k * n);
+  double* d = (double*)malloc(sizeof(double) * (size_t)m * n);
+  int ran = maxiter;
+  for (int iter = 1; iter <= maxiter; ++iter) {
+    memcpy(W0, W, sizeof(double) * (size_t)m * k);
+    memcpy(H0, H, sizeof(double) * (size_t)k * n);
+    orc_nmf_mu(A, W, H, m, n, k, 1, ORC_STOP_FIXED);
+    const double dnorm = orc_calculate_norm(A, W, H, d, m, n, k);
+    const double dw = orc_calculate_maxchange(W, W0, m, k, sqrteps);
+    const double dh = orc_calculate_maxchange(H, H0, k, n, sqrteps);
+    const double delta = (dh > dw) ? dh : dw;
+    const double dnorm0 = dnorm;
+    if (iter > 1 && iter % 2 == 0) {
+      if (delta < TolX) {
+        ran = iter;
+        break;
+      } else if (dnorm <= TolFun * dnorm0) {
+        ran = iter;
+        break;
+      }
+    }
+  }
+  free(W0);
+  free(H0);
+  free(d);
+  return ran;
 }

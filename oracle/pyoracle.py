@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libnmf_ref.so")
 
-STOP_FIXED, STOP_REF_COMPAT, STOP_ARGMAX_STABLE = 0, 1, 2
+STOP_FIXED, STOP_REF_COMPAT, STOP_ARGMAX_STABLE, STOP_TOLX = 0, 1, 2, 3
 LABEL_ARGMAX, LABEL_R_ORDER = 0, 1
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -62,6 +62,9 @@ class Oracle:
         L.orc_calculate_norm.restype = ctypes.c_double
         L.orc_calculate_maxchange.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_double]
         L.orc_calculate_maxchange.restype = ctypes.c_double
+        L.orc_nmf_mu_tol.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_double, ctypes.c_double]
+        L.orc_nmf_mu_tol.restype = ctypes.c_int
         # Brunet KL-divergence MU (brunet_oracle.c; parity unpinned vs the reference, see its header)
         L.orc_rmt_seed.argtypes = [ctypes.POINTER(_RMTState), ctypes.c_uint32]
         L.orc_rmt_unif.argtypes = [ctypes.POINTER(_RMTState)]
@@ -114,6 +117,16 @@ class Oracle:
         m, n = A.shape
         k = W.shape[1]
         it = self.L.orc_nmf_mu(_d(A), _d(W), _d(H), m, n, k, maxiter, stop_rule)
+        return W, H, it
+
+    def nmf_mu_tol(self, A, W, H, maxiter: int, TolX: float = 1e-4, TolFun: float = 1e-4):
+        """MU under the nmf_als.c:304-349 TolX/TolFun test -> (W, H, iterations)."""
+        A = np.asfortranarray(A, dtype=np.float64)
+        W = np.array(W, dtype=np.float64, order="F", copy=True)
+        H = np.array(H, dtype=np.float64, order="F", copy=True)
+        m, n = A.shape
+        k = W.shape[1]
+        it = self.L.orc_nmf_mu_tol(_d(A), _d(W), _d(H), m, n, k, maxiter, TolX, TolFun)
         return W, H, it
 
     def labels(self, H: np.ndarray, rule: int = LABEL_ARGMAX) -> np.ndarray:

@@ -217,3 +217,21 @@ def test_full_size_c3_shape_vs_oracle(oracle):
     W0, H0 = oracle.init_restart(20261015, m, n, k)
     Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, T, 0)
     assert relfro(r.W[0], Wo) < TOL and relfro(r.H[0], Ho) < TOL
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 5])
+def test_tolx_stop_rule(gct_engine, golden, k):
+    """NMFC_STOP_TOLX: calculateMaxchange-based stop, nmf_als.c:304-349 pattern."""
+    from pyoracle import Oracle
+    O = Oracle()
+    A = golden["A_gct"]
+    r = gct_engine.run([k], 1, maxiter=5000, seed=123, stop_rule=3, TolX=1e-3, want_factors=True, want_counts=False)
+    W0, H0 = O.init_restart(123, A.shape[0], A.shape[1], k)
+    Wo, Ho, it = O.nmf_mu_tol(A, W0, H0, 5000, 1e-3, 1e-4)
+    assert r.iters[0] == it and r.stopped_early[0] == (it < 5000)
+    assert relfro(r.W[0], Wo) < TOL and relfro(r.H[0], Ho) < TOL
+
+
+def test_tolx_tolfun_ge_one_stops_at_first_check(gct_engine):
+    r = gct_engine.run([2, 3], 2, maxiter=100, seed=9, stop_rule=3, TolX=0.0, TolFun=1.0, want_counts=False)
+    assert list(r.iters) == [2, 2, 2, 2]

@@ -87,3 +87,23 @@ def test_norm_maxchange(golden, oracle):
 def test_golden_labels_have_margin(golden):
     # labels are only meaningful as a bit-exact target when no column is a near-tie
     assert golden["c1_margin_argmax"].min() > 1e-6
+
+
+def test_tolx_rule_oracle(oracle, golden):
+    """orc_nmf_mu_tol: the nmf_als.c:304-349 convergence test around the MU update."""
+    A = golden["A_gct"]
+    W0, H0 = oracle.init_restart(123, A.shape[0], A.shape[1], 3)
+    # TolX = 0 never fires and TolFun < 1 only on an exactly-zero residual: plain fixed iterations
+    W, H, it = oracle.nmf_mu_tol(A, W0, H0, 20, 0.0, 1e-4)
+    Wf, Hf, _ = oracle.nmf_mu(A, W0, H0, 20, 0)
+    assert it == 20 and np.array_equal(W, Wf) and np.array_equal(H, Hf)
+    # TolFun >= 1: dnorm <= TolFun * dnorm0 with dnorm0 == dnorm holds at the first check (iteration 2)
+    assert oracle.nmf_mu_tol(A, W0, H0, 100, 0.0, 1.0)[2] == 2
+    # a real TolX stop: even, and the max-change at that iteration is below TolX (NumPy restatement)
+    W, H, it = oracle.nmf_mu_tol(A, W0, H0, 5000, 1e-3, 1e-4)
+    assert 2 < it < 5000 and it % 2 == 0
+    Wp, Hp, _ = oracle.nmf_mu(A, W0, H0, it - 1, 0)
+    sq = 2.0 ** -26.5
+    dw = np.max(np.abs(Wp - W)) / (sq + np.max(np.abs(Wp)))
+    dh = np.max(np.abs(Hp - H)) / (sq + np.max(np.abs(Hp)))
+    assert max(dw, dh) < 1e-3

@@ -329,7 +329,7 @@ int main(int argc, char** argv) {
   AHTW_VAR(3, "no W store")
   t = timeit([&] {
     hipLaunchKernelGGL(k_hupdate, dim3(nact), dim3(NT), 0, 0, 1, 10000, 0, dri, n, n_pad, Gpart, g_ld, g_split, nsplit,
-                       SWpart, sw_total, Hh, SH, stop, reason, unch, cls, 512L, nst, SHP, colact);
+                       SWpart, sw_total, Hh, SH, stop, reason, unch, cls, 512L, nst, SHP, colact, nullptr);
   }, reps);
   printf("k_hupdate    %8.3f ms\n", t);
   return 0;
