@@ -235,3 +235,20 @@ def test_tolx_stop_rule(gct_engine, golden, k):
 def test_tolx_tolfun_ge_one_stops_at_first_check(gct_engine):
     r = gct_engine.run([2, 3], 2, maxiter=100, seed=9, stop_rule=3, TolX=0.0, TolFun=1.0, want_counts=False)
     assert list(r.iters) == [2, 2, 2, 2]
+
+
+def test_full_size_c4_shape_vs_oracle(oracle):
+    """BASELINE config C4 shape (60000 x 2000), k = 2..15 batched, two fixed iterations: the k = 15 job
+    against the oracle, and every job bit-identical to its single-job run (batch invariance at size)."""
+    from nmfconsensus_amd.nmf import Engine
+    rng = np.random.default_rng(4)
+    m, n, T = 60000, 2000, 2
+    ks = list(range(2, 16))
+    A = np.asfortranarray(rng.random((m, n)) * 5.0)
+    with Engine(A) as eng:
+        r = eng.run(ks, 1, maxiter=T, seed=77, stop_rule=0, want_factors=True, want_counts=False)
+        single = eng.run([15], 1, maxiter=T, seed=77 + 13, stop_rule=0, want_factors=True, want_counts=False)
+    assert np.array_equal(r.W[13], single.W[0]) and np.array_equal(r.H[13], single.H[0])
+    W0, H0 = oracle.init_restart(77 + 13, m, n, 15)
+    Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, T, 0)
+    assert relfro(r.W[13], Wo) < TOL and relfro(r.H[13], Ho) < TOL
