@@ -93,8 +93,6 @@ struct Buf {
   }
 };
 
-// restarts per workgroup group: each lane keeps 4K doubles of state per restart (H or W row in,
-// accumulator out), so small k shares every A element over more restarts
 // q = a / p: rcp + two Newton steps + one residual correction (Markstein's final step), i.e. the
 // compiler's IEEE sequence without its operand-scaling steps (div_scale / div_fmas / div_fixup), which
 // only matter near the exponent limits.  Here a >= 0 and p is a positive rank-k product of
@@ -114,7 +112,17 @@ __device__ __forceinline__ double quot(double a, double p) {
 #endif
 }
 
-constexpr int rg_of(int K) { return K <= 2 ? 8 : K <= 3 ? 6 : K <= 4 ? 5 : K <= 5 ? 4 : K <= 6 ? 3 : K <= 10 ? 2 : 1; }
+// elements per lane: the LDS return path moves 8K bytes per lane for every element-restart's operand
+// row; where that (rather than the VALU work) bounds the kernel, each row serves 2 elements.  Measured
+// per k (tools/brunet_kbench.py, profiles/r01f_brunet_spl.txt): a gain for k = 8, 9 only -- elsewhere the
+// doubled register state costs more occupancy than the LDS traffic saves.
+constexpr int spl_of(int K) { return (K == 8 || K == 9) ? 2 : 1; }
+// restarts per workgroup: each lane keeps SPL * RG * 4K VGPRs of state (operand rows in, accumulators
+// out); RG shares every A element loaded over RG restarts
+constexpr int rg_of(int K) {
+  return spl_of(K) == 2 ? (K <= 6 ? 2 : 1)
+                        : (K <= 2 ? 8 : K <= 3 ? 6 : K <= 4 ? 5 : K <= 5 ? 4 : K <= 6 ? 3 : K <= 10 ? 2 : 1);
+}
 
 // ------------------------------------------------------------------------------------------------
 // Kernels
@@ -214,9 +222,10 @@ struct OperandTiles {
 };
 
 // H side, split over fixed gene chunks: Gp[chunk][b][c][j] = sum_{i in chunk} W[b][i][c] * A[i][j] / VP[i][j],
-// VP[i][j] = sum_c W[b][i][c] H[b][j][c].  Lane = sample j (H column and accumulator in registers);
-// W rows through the double-buffered LDS tiles.
-template <int K, int RG>
+// VP[i][j] = sum_c W[b][i][c] H[b][j][c].  Lane = SPL samples j (H columns and accumulators in
+// registers); W rows through the double-buffered LDS tiles.  A broadcast ds_read_b128 still moves
+// 1 KiB per wave through the LDS return path, so for larger k each W row read serves SPL = 2 samples.
+template <int K, int RG, int SPL>
 __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, long n_pad, int m, int n, int gc,
                                                 const int* __restrict__ act, int nact, const double* __restrict__ W,
                                                 long wstride, const double* __restrict__ H, long hstride,
@@ -224,23 +233,28 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
   using OT = OperandTiles<K, RG>;
   __shared__ double wl[2][OT::TW];
   __shared__ int sl[RG];
-  const int j = blockIdx.x * BT + threadIdx.x;
-  const int jl = j < n ? j : n - 1;
+  int jj[SPL], jl[SPL];
+#pragma unroll
+  for (int s = 0; s < SPL; ++s) {
+    jj[s] = blockIdx.x * (BT * SPL) + s * BT + threadIdx.x;
+    jl[s] = jj[s] < n ? jj[s] : n - 1;
+  }
   const int chunk = blockIdx.y;
   const int g0 = blockIdx.z * RG;
   const int nlive = min(RG, nact - g0);
   const int i0 = chunk * gc, i1 = min(m, i0 + gc);
   if (threadIdx.x < RG) sl[threadIdx.x] = act[min(g0 + (int)threadIdx.x, nact - 1)];
   __syncthreads();
-  double h[RG][K], g[RG][K];
+  double h[SPL][RG][K], g[SPL][RG][K];
 #pragma unroll
-  for (int r = 0; r < RG; ++r) {
+  for (int s = 0; s < SPL; ++s)
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-      h[r][c] = H[(long)sl[r] * hstride + (long)jl * K + c];
-      g[r][c] = 0.0;
-    }
-  }
+    for (int r = 0; r < RG; ++r)
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        h[s][r][c] = H[(long)sl[r] * hstride + (long)jl[s] * K + c];
+        g[s][r][c] = 0.0;
+      }
   OT ot;
   ot.fetch(W, wstride, sl, i0, i1);
   ot.store(wl[0]);
@@ -249,23 +263,28 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
   for (int t0 = i0; t0 < i1; t0 += TL, buf ^= 1) {
     const bool more = t0 + TL < i1;
     if (more) ot.fetch(W, wstride, sl, t0 + TL, i1);
-    const double* ap = Arm + (long)t0 * n_pad + jl;
+    const double* ap = Arm + (long)t0 * n_pad;
     const double* wt = wl[buf];
     // slots past the live restarts repeat the last live one (computed, never stored): no branches here
     auto gene = [&](int ii) {
-      const double a = ap[(long)ii * n_pad];
+      double a[SPL];
+#pragma unroll
+      for (int s = 0; s < SPL; ++s) a[s] = ap[(long)ii * n_pad + jl[s]];
 #pragma unroll
       for (int r = 0; r < RG; ++r) {
         const double* wr = wt + r * (TL * K) + ii * K;
         double w[K];
 #pragma unroll
         for (int c = 0; c < K; ++c) w[c] = wr[c];
-        double p = 0.0;
 #pragma unroll
-        for (int c = 0; c < K; ++c) p = fma(w[c], h[r][c], p);
-        const double q = quot(a, p);
+        for (int s = 0; s < SPL; ++s) {
+          double p = 0.0;
 #pragma unroll
-        for (int c = 0; c < K; ++c) g[r][c] = fma(w[c], q, g[r][c]);
+          for (int c = 0; c < K; ++c) p = fma(w[c], h[s][r][c], p);
+          const double q = quot(a[s], p);
+#pragma unroll
+          for (int c = 0; c < K; ++c) g[s][r][c] = fma(w[c], q, g[s][r][c]);
+        }
       }
     };
     if (i1 - t0 >= TL) {
@@ -277,14 +296,16 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
     if (more) ot.store(wl[buf ^ 1]);
     __syncthreads();
   }
-  if (j < n) {
 #pragma unroll
-    for (int r = 0; r < RG; ++r)
-      if (r < nlive) {
+  for (int s = 0; s < SPL; ++s)
+    if (jj[s] < n) {
 #pragma unroll
-        for (int c = 0; c < K; ++c) Gp[(long)chunk * gp_cs + ((long)sl[r] * K + c) * n_pad + j] = g[r][c];
-      }
-  }
+      for (int r = 0; r < RG; ++r)
+        if (r < nlive) {
+#pragma unroll
+          for (int c = 0; c < K; ++c) Gp[(long)chunk * gp_cs + ((long)sl[r] * K + c) * n_pad + jj[s]] = g[s][r][c];
+        }
+    }
 }
 
 template <int K>
@@ -366,9 +387,9 @@ __global__ __launch_bounds__(BT) void k_br_hupd(int t, int check, int stopconv, 
   }
 }
 
-// W side: lane = gene i over every sample j: F[i][c] = sum_j A[i][j] / VP[i][j] * H[j][c] with the new H
-// (LDS tiles of TL samples) and the old W row in registers; W <- (W * F + eps) / rowSums(H).
-template <int K, int RG>
+// W side: lane = SPL genes i over every sample j: F[i][c] = sum_j A[i][j] / VP[i][j] * H[j][c] with the
+// new H (LDS tiles of TL samples) and the old W rows in registers; W <- (W * F + eps) / rowSums(H).
+template <int K, int RG, int SPL>
 __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, long m_pad, int m, int n,
                                                 const int* __restrict__ act, int nact, double* __restrict__ W,
                                                 long wstride, const double* __restrict__ H, long hstride,
@@ -376,21 +397,26 @@ __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, 
   using OT = OperandTiles<K, RG>;
   __shared__ double hl[2][OT::TW];
   __shared__ int sl[RG];
-  const int i = blockIdx.x * BT + threadIdx.x;
-  const int il = i < m ? i : m - 1;
+  int ig[SPL], il[SPL];
+#pragma unroll
+  for (int s = 0; s < SPL; ++s) {
+    ig[s] = blockIdx.x * (BT * SPL) + s * BT + threadIdx.x;
+    il[s] = ig[s] < m ? ig[s] : m - 1;
+  }
   const int g0 = blockIdx.y * RG;
   const int nlive = min(RG, nact - g0);
   if (threadIdx.x < RG) sl[threadIdx.x] = act[min(g0 + (int)threadIdx.x, nact - 1)];
   __syncthreads();
-  double w[RG][K], f[RG][K];
+  double w[SPL][RG][K], f[SPL][RG][K];
 #pragma unroll
-  for (int r = 0; r < RG; ++r) {
+  for (int s = 0; s < SPL; ++s)
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-      w[r][c] = W[(long)sl[r] * wstride + (long)il * K + c];
-      f[r][c] = 0.0;
-    }
-  }
+    for (int r = 0; r < RG; ++r)
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        w[s][r][c] = W[(long)sl[r] * wstride + (long)il[s] * K + c];
+        f[s][r][c] = 0.0;
+      }
   OT ot;
   ot.fetch(H, hstride, sl, 0, n);
   ot.store(hl[0]);
@@ -399,22 +425,27 @@ __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, 
   for (int s0 = 0; s0 < n; s0 += TL, buf ^= 1) {
     const bool more = s0 + TL < n;
     if (more) ot.fetch(H, hstride, sl, s0 + TL, n);
-    const double* ap = Acm + (long)s0 * m_pad + il;
+    const double* ap = Acm + (long)s0 * m_pad;
     const double* ht = hl[buf];
     auto sample = [&](int jj) {
-      const double a = ap[(long)jj * m_pad];
+      double a[SPL];
+#pragma unroll
+      for (int s = 0; s < SPL; ++s) a[s] = ap[(long)jj * m_pad + il[s]];
 #pragma unroll
       for (int r = 0; r < RG; ++r) {
         const double* hj = ht + r * (TL * K) + jj * K;
         double hh[K];
 #pragma unroll
         for (int c = 0; c < K; ++c) hh[c] = hj[c];
-        double p = 0.0;
 #pragma unroll
-        for (int c = 0; c < K; ++c) p = fma(w[r][c], hh[c], p);
-        const double q = quot(a, p);
+        for (int s = 0; s < SPL; ++s) {
+          double p = 0.0;
 #pragma unroll
-        for (int c = 0; c < K; ++c) f[r][c] = fma(q, hh[c], f[r][c]);
+          for (int c = 0; c < K; ++c) p = fma(w[s][r][c], hh[c], p);
+          const double q = quot(a[s], p);
+#pragma unroll
+          for (int c = 0; c < K; ++c) f[s][r][c] = fma(q, hh[c], f[s][r][c]);
+        }
       }
     };
     if (n - s0 >= TL) {
@@ -426,16 +457,18 @@ __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, 
     if (more) ot.store(hl[buf ^ 1]);
     __syncthreads();
   }
-  if (i < m) {
 #pragma unroll
-    for (int r = 0; r < RG; ++r)
-      if (r < nlive) {
+  for (int s = 0; s < SPL; ++s)
+    if (ig[s] < m) {
 #pragma unroll
-        for (int c = 0; c < K; ++c)
-          W[(long)sl[r] * wstride + (long)i * K + c] =
-              __dadd_rn(__dmul_rn(w[r][c], f[r][c]), EPS) / RS[(long)sl[r] * K + c];
-      }
-  }
+      for (int r = 0; r < RG; ++r)
+        if (r < nlive) {
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+            W[(long)sl[r] * wstride + (long)ig[s] * K + c] =
+                __dadd_rn(__dmul_rn(w[s][r][c], f[s][r][c]), EPS) / RS[(long)sl[r] * K + c];
+        }
+    }
 }
 
 // labels[b][j] = order(H[,j], decreasing = TRUE)[1] (first row of the column maximum, 1-based)
@@ -575,6 +608,7 @@ template <int K>
 int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o, std::vector<int>& iters,
                std::vector<int>& stopped) {
   constexpr int RG = rg_of(K);
+  constexpr int SPL = spl_of(K);
   const int m = e->m, n = e->n;
   hipStream_t st = L->st;
   const long wstride = (long)m * K, hstride = (long)n * K;
@@ -592,7 +626,7 @@ int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o
     const int groups = (nact + RG - 1) / RG;
     {
       BTimed tl(L, BK_HNUM, fl * nact);
-      hipLaunchKernelGGL((k_br_hnum<K, RG>), dim3((n + BT - 1) / BT, e->nchunks, groups), dim3(BT), 0, st,
+      hipLaunchKernelGGL((k_br_hnum<K, RG, SPL>), dim3((n + BT * SPL - 1) / (BT * SPL), e->nchunks, groups), dim3(BT), 0, st,
                          e->Arm.as<double>(), e->n_pad, m, n, e->gc, L->act.as<int>(), nact, L->W.as<double>(), wstride,
                          L->H.as<double>(), hstride, L->Gp.as<double>(), gp_cs);
     }
@@ -604,7 +638,7 @@ int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o
     }
     {
       BTimed tl(L, BK_WUPD, fl * nact);
-      hipLaunchKernelGGL((k_br_wupd<K, RG>), dim3((m + BT - 1) / BT, groups), dim3(BT), 0, st, e->Acm.as<double>(),
+      hipLaunchKernelGGL((k_br_wupd<K, RG, SPL>), dim3((m + BT * SPL - 1) / (BT * SPL), groups), dim3(BT), 0, st, e->Acm.as<double>(),
                          e->m_pad, m, n, L->act.as<int>(), nact, L->W.as<double>(), wstride, L->H.as<double>(), hstride,
                          L->RS.as<double>());
     }
