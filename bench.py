@@ -227,21 +227,29 @@ def main():
             kernels[name] = {"launches": acc[0], "avg_ms": avg_ms, "algo_flop_per_launch": fl,
                              "tflops": fl / (avg_ms * 1e-3) / 1e12}
         kernels["hupdate"] = {"launches": hupd[0], "avg_ms": hupd[1] / max(hupd[0], 1)}
+        # algorithmic HBM bytes per launch (each operand once): a restart of rank k takes part in
+        # `iters` launches; A h^T reads A, h (k n) and W0 (m k) and writes W (m k); W^T A reads A and
+        # W and writes G (k n).  Averaged over the same launches as `achieved`.
+        kcol = np.asarray(ks)[np.arange(jb, je) % nk]
+        colsum = float(sum(np.sum(kcol * it) for it in iters_all))
+        kernels["ahtw"]["algo_bytes_per_launch"] = 8.0 * (m * n + colsum * (2 * m + n) / ahtw[0])
+        kernels["wta"]["algo_bytes_per_launch"] = 8.0 * (m * n + colsum * (m + n) / wta[0])
         dom = max(("wta", "ahtw"), key=lambda s: kernels[s]["avg_ms"] * kernels[s]["launches"])
         ach = kernels[dom]["tflops"]
         roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None, "kernels": kernels}
         # HBM bytes per launch of the dominant kernel from the committed PMC passes
         # (tools/profile_round.sh: FETCH_SIZE x 2 + WRITE_SIZE, full-load launches)
-        tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        tp = os.path.join(ROOT, "profiles", "r01g", "pmc_traffic.json")
         if os.path.exists(tp) and args.config == "C3":
             try:
                 pm = json.load(open(tp))
                 key = "k_wta2" if dom == "wta" else "k_ahtw4"
                 if key in pm:
                     roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
+                    roof["algo_bytes_per_launch"] = kernels[dom]["algo_bytes_per_launch"]
                     roof["traffic_unit"] = ("HBM bytes per launch, averaged over every launch of one C3 sweep like "
-                                            "`achieved` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_traffic.json)")
+                                            "`achieved` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r01g/pmc_traffic.json)")
             except Exception as ex:
                 log(f"[bench] could not read {tp}: {ex!r}")
 

@@ -1130,8 +1130,15 @@ static __global__ __launch_bounds__(NT, 2) void k_ahtw_t(int iter, const double*
 // B operand is exactly those registers (rows 4q..4q+3 of the D layout are the B fragment of k-step q).
 // The panel's h h^T blocks and column info are staged in LDS before the main loop.
 // ---------------------------------------------------------------------------------------------
+#ifndef NMFC_AHTW_SP
+#define NMFC_AHTW_SP 32
+#endif
+#ifndef NMFC_AHTW_SG
+#define NMFC_AHTW_SG 4
+#endif
 __device__ __forceinline__ void ahtw_map(int item, int npanels, int ngt, int& p, int& gt) {
-  const int SP = 8, SG = 8;   // bands of 8 panels, gene super-tiles of 8: neighbours share operands in L2
+  // bands of SP panels, gene super-tiles of SG: neighbours share operands in L2
+  const int SP = NMFC_AHTW_SP, SG = NMFC_AHTW_SG;
   const int band = item / (SP * ngt);
   const int rem = item % (SP * ngt);
   const int bp = min(SP, npanels - band * SP);
