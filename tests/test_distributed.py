@@ -63,6 +63,26 @@ def test_shard_ranges_cover_jobs():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_weak_scaling_shards_are_the_per_gpu_workload():
+    """bench.py --scaling weak: the job grid has R x N restarts per k and each of the N ranks gets one
+    contiguous block that holds exactly R restarts of every k (the N = 1 workload, distinct seeds)."""
+    from nmfconsensus_amd.distributed import shard_range
+    ks, R = list(range(2, 11)), 200
+    nk = len(ks)
+    for world in (1, 2, 4, 8):
+        seen = set()
+        for rank in range(world):
+            jb, je = shard_range(nk * R * world, rank, world)
+            jobs = np.arange(jb, je)
+            assert je - jb == nk * R
+            per_k = np.bincount(jobs % nk, minlength=nk)        # expand.grid: k fastest
+            assert (per_k == R).all()
+            restarts = jobs // nk
+            assert restarts.min() == rank * R and restarts.max() == (rank + 1) * R - 1
+            seen.update(jobs.tolist())
+        assert seen == set(range(nk * R * world))
+
+
 @pytest.mark.timeout(300)
 def test_gloo_world2_counts_equal_golden(golden):
     ctx = mp.get_context("spawn")
