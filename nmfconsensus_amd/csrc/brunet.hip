@@ -118,10 +118,31 @@ __device__ __forceinline__ double quot(double a, double p) {
 // doubled register state costs more occupancy than the LDS traffic saves.
 constexpr int spl_of(int K) { return (K == 8 || K == 9) ? 2 : 1; }
 // restarts per workgroup: each lane keeps SPL * RG * 4K VGPRs of state (operand rows in, accumulators
-// out); RG shares every A element loaded over RG restarts
+// out); RG shares every A element loaded over RG restarts.  Per-k values measured on the C5 shape
+// (profiles/r01g/brunet_rg/): the best RG is not monotone in k because register-count occupancy
+// steps and grid size (groups = R / RG) move together; RG never changes a restart's arithmetic.
+#ifndef NMFC_BR_RG2
+#define NMFC_BR_RG2 5
+#endif
+#ifndef NMFC_BR_RG3
+#define NMFC_BR_RG3 4
+#endif
+#ifndef NMFC_BR_RG4
+#define NMFC_BR_RG4 5
+#endif
+#ifndef NMFC_BR_RG5
+#define NMFC_BR_RG5 4
+#endif
+#ifndef NMFC_BR_RG6
+#define NMFC_BR_RG6 2
+#endif
+#ifndef NMFC_BR_RG7
+#define NMFC_BR_RG7 2
+#endif
 constexpr int rg_of(int K) {
   return spl_of(K) == 2 ? (K <= 6 ? 2 : 1)
-                        : (K <= 2 ? 8 : K <= 3 ? 6 : K <= 4 ? 5 : K <= 5 ? 4 : K <= 6 ? 3 : K <= 10 ? 2 : 1);
+                        : (K <= 2 ? NMFC_BR_RG2 : K <= 3 ? NMFC_BR_RG3 : K <= 4 ? NMFC_BR_RG4 : K <= 5 ? NMFC_BR_RG5
+                           : K <= 6 ? NMFC_BR_RG6 : K <= 7 ? NMFC_BR_RG7 : K <= 10 ? 2 : 1);
 }
 
 // ------------------------------------------------------------------------------------------------
