@@ -240,7 +240,7 @@ def main():
                 "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None, "kernels": kernels}
         # HBM bytes per launch of the dominant kernel from the committed PMC passes
         # (tools/profile_round.sh: FETCH_SIZE x 2 + WRITE_SIZE, full-load launches)
-        tp = os.path.join(ROOT, "profiles", "r01g", "pmc_traffic.json")
+        tp = os.path.join(ROOT, "profiles", "r01h", "pmc_traffic.json")
         if os.path.exists(tp) and args.config == "C3":
             try:
                 pm = json.load(open(tp))
@@ -249,7 +249,7 @@ def main():
                     roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
                     roof["algo_bytes_per_launch"] = kernels[dom]["algo_bytes_per_launch"]
                     roof["traffic_unit"] = ("HBM bytes per launch, averaged over every launch of one C3 sweep like "
-                                            "`achieved` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r01g/pmc_traffic.json)")
+                                            "`achieved` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r01h/pmc_traffic.json)")
             except Exception as ex:
                 log(f"[bench] could not read {tp}: {ex!r}")
 

@@ -297,7 +297,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   }
   if (const char* s = getenv("NMFC_WTA_TILE")) {
     const std::string v(s);
-    e->force_wta = v == "big" ? 0 : v == "small" ? 1 : v == "tiny" ? 2 : -1;
+    e->force_wta = v == "big" ? 0 : v == "small" ? 1 : v == "tiny" ? 2 : v == "mid" ? 3 : -1;
   }
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
     const std::string v(s);
@@ -582,12 +582,15 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       const int chunk = std::min(opts.check_every, opts.maxiter - it);
       // tile shapes by grid size (a speed choice only: every shape sums in the canonical K order)
       bool wta_big = (long)e->nsplit * (pk.npanels / WTA_NPT) * ntj >= 2L * e->ncu;
-      bool wta_tiny = !wta_big && (long)e->nsplit * pk.npanels * 2 * ntj <= 2L * e->ncu;
+      // 2-panel x 128-sample tiles (8 waves) while they still give every CU a workgroup
+      bool wta_mid = !wta_big && (long)e->nsplit * (pk.npanels / 2) * ntj >= (long)e->ncu;
+      bool wta_tiny = !wta_big && !wta_mid && (long)e->nsplit * pk.npanels * 2 * ntj <= 2L * e->ncu;
       // A h^T tiles: 1 panel x 128 genes, or 1 panel x 64 genes for small grids (twice the workgroups)
       bool ahtw_small = (long)pk.npanels * e->ngt <= 8L * e->ncu;
       if (e->force_wta >= 0) {   // NMFC_WTA_TILE (tests: every shape must give the same bits)
         wta_big = e->force_wta == 0;
         wta_tiny = e->force_wta == 2;
+        wta_mid = e->force_wta == 3;
       }
       if (e->force_ahtw >= 0) ahtw_small = e->force_ahtw == 1;
       const int ngt_ahtw = e->ngt * (ahtw_small ? 2 : 1);
@@ -603,6 +606,14 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
             const int ng = pk.npanels / WTA_NPT;
             auto kw = (ntj >= 4) ? k_wta2<WTA_NPT, 128, 4, 2, 1> : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2>
                                                                             : k_wta2<WTA_NPT, 128, 4, 2, 4>;
+            hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
+                               e->Acm.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
+                               e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
+                               e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
+                               sw_total);
+          } else if (wta_mid) {   // npanels is a multiple of WTA_NPT, so of 2
+            const int ng = pk.npanels / 2;
+            auto kw = (ntj >= 2) ? k_wta2<2, 128, 4, 2, 1> : k_wta2<2, 128, 4, 2, 2>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
                                e->Acm.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
