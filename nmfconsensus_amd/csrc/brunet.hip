@@ -144,6 +144,17 @@ constexpr int rg_of(int K) {
                         : (K <= 2 ? NMFC_BR_RG2 : K <= 3 ? NMFC_BR_RG3 : K <= 4 ? NMFC_BR_RG4 : K <= 5 ? NMFC_BR_RG5
                            : K <= 6 ? NMFC_BR_RG6 : K <= 7 ? NMFC_BR_RG7 : K <= 10 ? 2 : 1);
 }
+// small batches (B <= NMFC_BR_SMALL_B restarts of one k, e.g. one rank's shard of a strong-scaling
+// run): fewer restarts per workgroup so the batch still spreads over the CUs
+#ifndef NMFC_BR_SMALL_B
+#define NMFC_BR_SMALL_B 0
+#endif
+#ifndef NMFC_BR_RG_SMALL_DIV
+#define NMFC_BR_RG_SMALL_DIV 0
+#endif
+constexpr int rg_small(int K) {
+  return NMFC_BR_RG_SMALL_DIV == 0 ? 1 : (rg_of(K) / NMFC_BR_RG_SMALL_DIV > 1 ? rg_of(K) / NMFC_BR_RG_SMALL_DIV : 1);
+}
 
 // ------------------------------------------------------------------------------------------------
 // Kernels
@@ -625,10 +636,9 @@ struct nmfc_brunet {
 namespace {
 
 // one k: B restarts (slots 0..B-1) already initialised in L->W / L->H; iterates to the stop rule.
-template <int K>
+template <int K, int RG = rg_of(K)>
 int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o, std::vector<int>& iters,
                std::vector<int>& stopped) {
-  constexpr int RG = rg_of(K);
   constexpr int SPL = spl_of(K);
   const int m = e->m, n = e->n;
   hipStream_t st = L->st;
@@ -697,7 +707,8 @@ int br_dispatch(const nmfc_brunet* e, BrLane* L, int K, int B, const nmfc_brunet
   switch (K) {
 #define BR_CASE(KK) \
   case KK:          \
-    return br_iterate<KK>(e, L, B, o, iters, stopped);
+    return B <= NMFC_BR_SMALL_B ? br_iterate<KK, rg_small(KK)>(e, L, B, o, iters, stopped) \
+                                : br_iterate<KK>(e, L, B, o, iters, stopped);
     BR_CASE(2) BR_CASE(3) BR_CASE(4) BR_CASE(5) BR_CASE(6) BR_CASE(7) BR_CASE(8) BR_CASE(9) BR_CASE(10) BR_CASE(11)
     BR_CASE(12) BR_CASE(13) BR_CASE(14) BR_CASE(15) BR_CASE(16)
 #undef BR_CASE
