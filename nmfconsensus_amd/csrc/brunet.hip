@@ -147,7 +147,7 @@ constexpr int rg_of(int K) {
 // small batches (B <= NMFC_BR_SMALL_B restarts of one k, e.g. one rank's shard of a strong-scaling
 // run): fewer restarts per workgroup so the batch still spreads over the CUs
 #ifndef NMFC_BR_SMALL_B
-#define NMFC_BR_SMALL_B 0
+#define NMFC_BR_SMALL_B 32
 #endif
 #ifndef NMFC_BR_RG_SMALL_DIV
 #define NMFC_BR_RG_SMALL_DIV 0
