@@ -148,6 +148,8 @@ def main():
         return bench_brunet(args, rank, world, local, dev)
 
     m, n, ks, R, desc = CONFIGS[args.config]
+    if args.config == "C4" and args.scaling == "weak":
+        R = R // 8             # C4 is the 8-GPU job: 125 restarts of every k per GPU (at N = 8 the whole C4)
     if args.restarts:
         R = args.restarts
     if args.scaling == "weak":
