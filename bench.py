@@ -10,8 +10,10 @@ consensus = counts / R and the cophenetic correlation per k.  A is resident in H
   N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line.  value = restarts completed by all ranks / max-over-ranks wall time.
-Scaling: default "weak" -- every GPU runs the per-GPU workload (R restarts of
-every k; the job's consensus is over R x N restarts); "--scaling strong" splits the fixed R over N.
+Scaling: default "strong" -- the fixed job (R restarts of every k, BASELINE
+north_star: "k=2..10 x 200-restart consensus ... on 8 x MI355X") is split over the N GPUs; "--scaling
+weak" gives every GPU the whole per-GPU workload (the consensus is then over R x N restarts).  C4 is
+always the per-GPU share of BASELINE configs[3] (1000/8 restarts of every k per GPU, weak).
 """
 from __future__ import annotations
 
@@ -71,13 +73,28 @@ def _cpu_worker(args):
     return out
 
 
-def cpu_baseline(m, n, ks, mean_iters_per_k, cores, T, brunet=False):
+def host_cpu():
+    """CPU model and thread counts of the host the baseline ran on (state them)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+
+
+def cpu_baseline(m, n, ks, mean_iters_per_k, cores, T, brunet=False, kind="reference"):
     import multiprocessing as mp
 
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libnmf_ref.so")
     if brunet:
         kind = "brunet"
-    else:
-        kind = "reference" if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libnmf_ref.so")) else "port"
+    elif kind == "reference" and not os.path.exists(ref_so):
+        raise FileNotFoundError(f"cpu_baseline kind 'reference' needs {ref_so} (built by `make -C oracle ref` where "
+                                "/root/reference exists); pass --cpu-kind port to time the C restatement instead")
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
     devnull = os.open(os.devnull, os.O_WRONLY)
@@ -106,6 +123,7 @@ def cpu_baseline(m, n, ks, mean_iters_per_k, cores, T, brunet=False):
                    f" x {cores} concurrent processes, {T} iterations per k={ks[0]}..{ks[-1]} on the {m}x{n} matrix; "
                    f"restarts/s extrapolated with the GPU run's mean iterations per k; sample wall {wall:.1f} s"),
         "sec_per_iter": {str(k): t_iter[k] for k in ks},
+        "host": host_cpu(),
     }
 
 
@@ -122,9 +140,13 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=100, help="iterations per k in the CPU sample (~20 s wall on 16 cores)")
     ap.add_argument("--cpu-cores", type=int, default=None)
     ap.add_argument("--no-timing", action="store_true", help="disable per-launch HIP event timing")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: every GPU runs the full per-GPU workload (R restarts per k each, consensus over "
-                         "R x N); strong: the fixed R restarts per k are split over the N GPUs")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="strong (default): the fixed R restarts per k are split over the N GPUs (the north-star "
+                         "job); weak: every GPU runs the full per-GPU workload (R restarts per k each, consensus "
+                         "over R x N).  C4 is always weak (the per-GPU share of configs[3])")
+    ap.add_argument("--cpu-kind", default="reference", choices=["reference", "port"],
+                    help="reference: the reference's own nmf_mu (oracle/_ref, fails loudly when absent); port: the "
+                         "oracle's C restatement")
     args = ap.parse_args()
 
     import numpy as np
@@ -140,15 +162,18 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from nmfconsensus_amd.synthetic import CONFIGS, planted_matrix
-    from nmfconsensus_amd.nmf import Engine, cophenetic
+    from nmfconsensus_amd.nmf import Engine, cophenetic_batch
     from nmfconsensus_amd.distributed import shard_range
     from nmfconsensus_amd import _lib
 
+    if args.scaling is None:
+        args.scaling = "weak" if args.config == "C4" else "strong"
     if args.config == "C5":
         return bench_brunet(args, rank, world, local, dev)
 
     m, n, ks, R, desc = CONFIGS[args.config]
-    if args.config == "C4" and args.scaling == "weak":
+    if args.config == "C4":
+        args.scaling = "weak"
         R = R // 8             # C4 is the 8-GPU job: 125 restarts of every k per GPU (at N = 8 the whole C4)
     if args.restarts:
         R = args.restarts
@@ -166,16 +191,16 @@ def main():
     timing = not args.no_timing
 
     def step():
+        torch.cuda.current_stream().synchronize()   # the previous all-reduce has finished reading counts
         res = eng.run(ks, R, maxiter=args.maxiter, seed=123, stop_rule=stop_rule, job_begin=jb, job_end=je,
                       counts_device_ptr=counts.data_ptr(), check_every=16)
         if world > 1:
             torch.distributed.all_reduce(counts, op=torch.distributed.ReduceOp.SUM)
         cons = counts.to(torch.float64) / R
         rho = {}
-        if rank == 0:
-            C = cons.cpu().numpy()
-            for i, k in enumerate(ks):
-                rho[k] = cophenetic(C[i])[0]
+        if rank == 0:   # cophenetic correlation per k (nmf.r:165-172), the k's on parallel host threads
+            r = cophenetic_batch(cons.cpu().numpy())[0]
+            rho = {k: float(r[i]) for i, k in enumerate(ks)}
         return res, rho
 
     eng.set_timing(False)
@@ -186,22 +211,23 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    iters_all, wta = [], [0, 0.0, 0.0]
-    ahtw = [0, 0.0, 0.0]
-    hupd = [0, 0.0]
+    iters_all = []
+    # per kernel id: [launches, ms, flop*launches, design bytes*launches, algorithmic bytes*launches]
+    acc = {kid: [0, 0.0, 0.0, 0.0, 0.0] for kid in (_lib.KID_WTA, _lib.KID_AHTW, _lib.KID_HUPD, _lib.KID_LABELS,
+                                                     _lib.KID_COUNTS)}
     last = None
     for _ in range(args.steps):
         res, rho = step()
         last = (res, rho)
         iters_all.append(res.iters.copy())
-        for acc, kid in ((wta, _lib.KID_WTA), (ahtw, _lib.KID_AHTW)):
+        for kid, a in acc.items():
             c, ms = eng.kernel_time(kid)
-            acc[0] += c
-            acc[1] += ms
-            acc[2] += eng.kernel_flops(kid) * c
-        c, ms = eng.kernel_time(_lib.KID_HUPD)
-        hupd[0] += c
-        hupd[1] += ms
+            b, ab = eng.kernel_bytes(kid)
+            a[0] += c
+            a[1] += ms
+            a[2] += eng.kernel_flops(kid) * c
+            a[3] += b * c
+            a[4] += ab * c
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -216,56 +242,59 @@ def main():
     value = total_restarts / elapsed
     its = np.concatenate(iters_all)
     local_jobs = np.arange(jb, je)
-    mean_iter_k = {k: float(np.mean(res.iters[(local_jobs % nk) == i])) for i, k in enumerate(ks)}
+    mean_iter_k = {k: float(np.mean(res.iters[(local_jobs % nk) == i])) for i, k in enumerate(ks)
+                   if np.any((local_jobs % nk) == i)}
     log(f"[bench] rank {rank}: {je - jb} restarts/step, mean iters {its.mean():.1f} (max {its.max()}), "
         f"step {elapsed / args.steps:.3f} s, engine {res.seconds_total:.3f} s (iterate {res.seconds_iterate:.3f} s)")
 
     roof = None
-    kernels = {}
-    if timing and wta[0] and ahtw[0]:
-        for name, acc in (("wta", wta), ("ahtw", ahtw)):
-            avg_ms = acc[1] / acc[0]
-            fl = acc[2] / acc[0]
-            kernels[name] = {"launches": acc[0], "avg_ms": avg_ms, "algo_flop_per_launch": fl,
-                             "tflops": fl / (avg_ms * 1e-3) / 1e12}
-        kernels["hupdate"] = {"launches": hupd[0], "avg_ms": hupd[1] / max(hupd[0], 1)}
-        # algorithmic HBM bytes per launch (each operand once): a restart of rank k takes part in
-        # `iters` launches; A h^T reads A, h (k n) and W0 (m k) and writes W (m k); W^T A reads A and
-        # W and writes G (k n).  Averaged over the same launches as `achieved`.
-        kcol = np.asarray(ks)[np.arange(jb, je) % nk]
-        colsum = float(sum(np.sum(kcol * it) for it in iters_all))
-        kernels["ahtw"]["algo_bytes_per_launch"] = 8.0 * (m * n + colsum * (2 * m + n) / ahtw[0])
-        kernels["wta"]["algo_bytes_per_launch"] = 8.0 * (m * n + colsum * (m + n) / wta[0])
+    if timing and acc[_lib.KID_WTA][0] and acc[_lib.KID_AHTW][0]:
+        kernels = {}
+        names = {_lib.KID_WTA: "wta", _lib.KID_AHTW: "ahtw", _lib.KID_HUPD: "hupdate", _lib.KID_LABELS: "labels",
+                 _lib.KID_COUNTS: "counts"}
+        for kid, (c, ms, fl, b, ab) in acc.items():
+            if not c:
+                continue
+            avg_ms = ms / c
+            kr = {"launches": c, "avg_ms": avg_ms, "algo_bytes_per_launch": ab / c, "design_bytes_per_launch": b / c,
+                  "gbs": ab / c / (avg_ms * 1e-3) / 1e9, "design_gbs": b / c / (avg_ms * 1e-3) / 1e9}
+            kr["frac_hbm"] = kr["gbs"] / HBM_PEAK_GBS
+            if fl:
+                kr["algo_flop_per_launch"] = fl / c
+                kr["tflops"] = fl / c / (avg_ms * 1e-3) / 1e12
+                kr["bound"] = "mfma"
+                kr["frac"] = kr["tflops"] / FP64_MFMA_PEAK_TFLOPS
+            else:
+                kr["bound"] = "hbm"
+                kr["frac"] = kr["frac_hbm"]
+            kernels[names[kid]] = kr
+        if rank == 0:
+            kernels.update(side_kernels(A_dev, m, n, max(ks)))
         dom = max(("wta", "ahtw"), key=lambda s: kernels[s]["avg_ms"] * kernels[s]["launches"])
         ach = kernels[dom]["tflops"]
         roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None, "kernels": kernels}
-        # HBM bytes per launch of the dominant kernel from the committed PMC passes
-        # (tools/profile_round.sh: FETCH_SIZE x 2 + WRITE_SIZE, full-load launches)
-        tp = os.path.join(ROOT, "profiles", "r01h", "pmc_traffic.json")
-        if os.path.exists(tp) and args.config == "C3":
-            try:
-                pm = json.load(open(tp))
-                key = "k_wta2" if dom == "wta" else "k_ahtw4"
-                if key in pm:
-                    roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
-                    roof["algo_bytes_per_launch"] = kernels[dom]["algo_bytes_per_launch"]
-                    roof["traffic_unit"] = ("HBM bytes per launch, averaged over every launch of one C3 sweep like "
-                                            "`achieved` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r01h/pmc_traffic.json)")
-            except Exception as ex:
-                log(f"[bench] could not read {tp}: {ex!r}")
+                "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                "algo_bytes_per_launch": kernels[dom]["algo_bytes_per_launch"], "kernels": kernels,
+                "note": ("achieved = algorithmic flop per launch (SURVEY 8(d): 2mnk + 2mk^2 per live restart) / "
+                         "the kernel's mean HIP-event duration over every launch of the timed sweeps; kernels[*] "
+                         "with bound 'hbm': algorithmic bytes per launch / mean duration vs 8 TB/s")}
+        tp = pmc_profile_for(args.config, dom)
+        if tp:
+            roof["traffic"], roof["traffic_unit"] = tp
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
         try:
-            cpu = cpu_baseline(m, n, ks, mean_iter_k, cores, args.cpu_iters)
-        except Exception as ex:  # reported, never fatal for the GPU number
-            log(f"[bench] cpu baseline failed: {ex!r}")
+            cpu = cpu_baseline(m, n, ks, mean_iter_k, cores, args.cpu_iters, kind=args.cpu_kind)
+        except Exception as ex:  # reported loudly in the line and on stderr, never fatal for the GPU number
+            log(f"[bench] CPU BASELINE FAILED: {ex!r}")
+            cpu = {"value": None, "error": repr(ex), "kind": args.cpu_kind}
 
     if rank == 0:
+        per_gpu = R / world if args.scaling == "strong" else R // world
         out = {
-            "metric": "NMF restarts/sec (k=2..10 sweep, 20k×500 fp64) + fp64-MFMA/HBM roofline %",
+            "metric": metric_name(args.config, m, n, ks),
             "value": value,
             "unit": "restarts/s",
             "n_gpus": world,
@@ -277,9 +306,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (planted 4-group matrix, splitmix64 seed 20261015; per-job generateMatrix(ran) init)",
-            "config": {"workload": f"{args.config}: {desc}, stop rule {args.stop_rule}, maxiter {args.maxiter}",
-                       "m": m, "n": n, "ks": ks, "restarts_per_k": R, "restarts_per_k_per_gpu": R // world
-                       if args.scaling == "weak" else R / world, "jobs": nk * R,
+            "config": {"workload": (f"{args.config}: synthetic {m}x{n} fp64, k={ks[0]}..{ks[-1]}, {R} restarts per k "
+                                    f"({nk * R} jobs) in total, {per_gpu:g} restarts per k per GPU, stop rule "
+                                    f"{args.stop_rule}, maxiter {args.maxiter}"),
+                       "m": m, "n": n, "ks": ks, "restarts_per_k": R, "restarts_per_k_per_gpu": per_gpu,
+                       "jobs": nk * R,
                        "parallelism": f"jobs sharded over {world} GPU(s) ({args.scaling} scaling), "
                                       "RCCL int32 all-reduce of counts",
                        "mean_iterations": float(its.mean()), "max_iterations": int(its.max()),
@@ -291,6 +322,86 @@ def main():
     eng.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def metric_name(config, m, n, ks):
+    if config in ("C3", "C5"):   # BASELINE.json metric, verbatim
+        base = "NMF restarts/sec (k=2..10 sweep, 20k×500 fp64) + fp64-MFMA/HBM roofline %"
+        return base if config == "C3" else base.replace("NMF restarts", "Brunet KL-divergence NMF restarts")
+    return f"NMF restarts/sec (k={ks[0]}..{ks[-1]} sweep, {m}×{n} fp64) + fp64-MFMA/HBM roofline %"
+
+
+def side_kernels(A_dev, m, n, k, reps=3):
+    """HBM roofline of calculateNorm / calculateMaxchange (calculatenorm.c:58-66, calculatemaxchange.c:55-60)
+    on the config's A (device-resident) with W, H of rank k: the libnmf convergence reductions, run beside the
+    sweep (the reference's nmf_mu leaves them commented out, nmf_mu.c:220-237; the TOLX stop rule uses the
+    max-change form)."""
+    import ctypes
+    import torch
+    from nmfconsensus_amd import _lib
+
+    L = _lib.lib()
+    g = torch.Generator(device=A_dev.device).manual_seed(7)
+    W = torch.rand((k, m), dtype=torch.float64, device=A_dev.device, generator=g)   # (m x k) column-major
+    H = torch.rand((n, k), dtype=torch.float64, device=A_dev.device, generator=g)   # (k x n) column-major
+    D = torch.empty_like(A_dev)
+    M0 = torch.empty_like(A_dev)
+    torch.cuda.synchronize()
+    out = {}
+    v, ms = ctypes.c_double(0.0), ctypes.c_double(0.0)
+    t = []
+    for _ in range(reps):
+        rc = L.nmfc_calculate_norm_dev(A_dev.data_ptr(), W.data_ptr(), H.data_ptr(), D.data_ptr(), m, n, k,
+                                       ctypes.byref(v), ctypes.byref(ms))
+        if rc != 0:
+            return {}
+        t.append(ms.value)
+    ab = 16.0 * m * n + 8.0 * (m + n) * k    # A read, d written, W and H read once
+    avg = sum(t) / len(t)
+    out["norm"] = {"launches": reps, "avg_ms": avg, "algo_bytes_per_launch": ab, "gbs": ab / (avg * 1e-3) / 1e9,
+                   "bound": "hbm", "shape": f"{m}x{n}, k={k}"}
+    t = []
+    for _ in range(reps):
+        M0.copy_(A_dev)
+        torch.cuda.synchronize()
+        rc = L.nmfc_calculate_maxchange_dev(D.data_ptr(), M0.data_ptr(), m, n, 2.0 ** -26.5, ctypes.byref(v),
+                                            ctypes.byref(ms))
+        if rc != 0:
+            return out
+        t.append(ms.value)
+    ab = 24.0 * m * n                        # mat, mat0 read, mat0 written
+    avg = sum(t) / len(t)
+    out["maxchange"] = {"launches": reps, "avg_ms": avg, "algo_bytes_per_launch": ab,
+                        "gbs": ab / (avg * 1e-3) / 1e9, "bound": "hbm", "shape": f"{m}x{n}"}
+    for kr in out.values():
+        kr["frac_hbm"] = kr["frac"] = kr["gbs"] / HBM_PEAK_GBS
+        kr["design_bytes_per_launch"], kr["design_gbs"] = kr["algo_bytes_per_launch"], kr["gbs"]
+    return out
+
+
+def pmc_profile_for(config, dom):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC passes (tools/profile_round.sh:
+    FETCH_SIZE x 2 + WRITE_SIZE) -- used only when the profile was taken on THIS kernel source (its recorded
+    source hash matches), so the figure cannot go stale silently."""
+    from nmfconsensus_amd.build import source_sha256
+
+    if config != "C3":
+        return None
+    import glob
+    sha = source_sha256()
+    key = "k_wta2" if dom == "wta" else "k_ahtw4"
+    for tp in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+        try:
+            pm = json.load(open(tp))
+        except Exception:
+            continue
+        if pm.get("source_sha256") != sha or key not in pm:
+            continue
+        return (pm[key]["hbm_bytes_per_launch"],
+                "HBM bytes per launch, averaged over every launch of one C3 sweep like `achieved` (rocprofv3 "
+                f"FETCH_SIZE x2 + WRITE_SIZE, {os.path.relpath(tp, ROOT)}, same kernel source)")
+    log("[bench] no committed PMC profile matches this kernel source: roofline.traffic = null")
+    return None
 
 
 def bench_brunet(args, rank, world, local, dev):

@@ -29,6 +29,14 @@ enum {
                                    TolFun >= 1 (dnorm <= TolFun * dnorm0 with dnorm0 == dnorm, :330/:345) */
 };
 
+/* Initialisation streams of the per-job W0/H0. */
+enum {
+  NMFC_INIT_LIBNMF = 0,         /* libnmf generateMatrix(ran): glibc rand() after srand(job seed)
+                                   (generatematrix.c:94-100, randnumber.c:27-35; the north-star stream) */
+  NMFC_INIT_R_RUNIF = 1         /* nmf.r:37-38: set.seed(job seed); W <- runif(m*k); H <- runif(k*n)
+                                   (R's Mersenne-Twister; BatchJobs job seed = seed + job_id - 1) */
+};
+
 /* Label rules for the consensus (nmf.r:128). */
 enum {
   NMFC_LABEL_ARGMAX = 0,        /* row of the column maximum (nmf.r:127 comment, BROAD intent) */
@@ -48,6 +56,7 @@ typedef struct nmfc_sweep_opts {
   int verbose;        /* 0 quiet; 1 per-sweep summary on stderr */
   double TolX;        /* NMFC_STOP_TOLX threshold (options_t.TolX, default 1e-4, setdefaultopts.c) */
   double TolFun;      /* NMFC_STOP_TOLX TolFun (default 1e-4) */
+  int init_stream;    /* NMFC_INIT_* (default NMFC_INIT_LIBNMF; min_init/max_init apply to LIBNMF only) */
 } nmfc_sweep_opts;
 
 /* Outputs.  Every pointer may be NULL.  Host memory unless *_on_device is set.
@@ -101,6 +110,12 @@ int nmfc_consensus(const double* Hs, int k, int n, int R, int label_rule, int32_
  * leaf order (HC$order); merge_out (2*(n-1), may be NULL) R-style merge matrix; height_out (n-1). */
 double nmfc_cophenetic(const double* C, int n, int32_t* order_out, int32_t* merge_out, double* height_out);
 
+/* nmfc_cophenetic for nk consensus matrices (nk x n x n, each column-major) on up to nthreads host threads
+ * (<= 0: all hardware threads); rho_out[nk]; order_out (nk x n), merge_out (nk x 2(n-1)), height_out
+ * (nk x (n-1)) may be NULL.  Returns 0, or -1 on bad arguments. */
+int nmfc_cophenetic_batch(const double* C, int nk, int n, int nthreads, double* rho_out, int32_t* order_out,
+                          int32_t* merge_out, double* height_out);
+
 /* cutree(HC, k) membership (nmf.r:177) from a merge matrix produced by nmfc_cophenetic. 1-based. */
 int nmfc_cutree(const int32_t* merge, int n, int k, int32_t* membership_out);
 
@@ -138,17 +153,31 @@ void nmfc_brunet_set_timing(nmfc_brunet* e, int enable);
  * (k_br_wupd); returns launches, fills accumulated event ms and algorithmic flop per launch. */
 long long nmfc_brunet_kernel_time(nmfc_brunet* e, int kernel_id, double* ms_out, double* flops_per_launch);
 
+/* calculateNorm (calculatenorm.c:44-78) and calculateMaxchange (calculatemaxchange.c:42-71) on
+ * DEVICE-resident column-major operands (e.g. torch tensors) on the current HIP device: d = a - w h and
+ * *norm_out = ||d||_F / sqrt(m n); *out = max|mat0 - mat| / (sqrteps + max|mat0|) with mat0 -= mat.
+ * ms_out (may be NULL) receives the device time of the reduction pass.  Return 0, or -1 on failure. */
+int nmfc_calculate_norm_dev(const double* a, const double* w, const double* h, double* d, int m, int n, int k,
+                            double* norm_out, double* ms_out);
+int nmfc_calculate_maxchange_dev(const double* mat, double* mat0, int m, int n, double sqrteps, double* out,
+                                 double* ms_out);
+
 /* Diagnostics. */
 const char* nmfc_last_error(void);
 const char* nmfc_version(void);
 /* Per-kernel device time (ms) accumulated over the last run, measured with HIP events on the
- * engine's stream: kernel ids 0 = wta (W^T[A|W] MFMA), 1 = hupdate, 2 = ahtw (A H^T MFMA + W update),
- * 3 = init, 4 = labels+counts.  Returns the number of launches of that kernel. */
+ * engine's stream: kernel ids 0 = wta (W^T A + W^T W, MFMA), 1 = hupdate (H update + stop check),
+ * 2 = ahtw (A h^T MFMA + W update), 3 = init, 4 = other (repack moves, TolX W check), 5 = labels,
+ * 6 = connectivity counts.  Returns the number of launches of that kernel. */
 long long nmfc_engine_kernel_time(nmfc_engine* e, int kernel_id, double* ms_out);
 /* Enables per-launch event timing (adds small overhead; used by bench.py's roofline leg). */
 void nmfc_engine_set_timing(nmfc_engine* e, int enable);
 /* Algorithmic flop per launch of the dominant kernel in the last run, for the roofline report. */
 double nmfc_engine_kernel_flops(nmfc_engine* e, int kernel_id);
+/* HBM bytes per launch in the last run: returns the bytes the kernel's design moves (operands once plus
+ * split-K / Gram partials); *algo_bytes_out (may be NULL) receives the algorithmic bytes (each operand
+ * once; the H update uses SURVEY 8(d)'s 32 n k per restart-iteration). */
+double nmfc_engine_kernel_bytes(nmfc_engine* e, int kernel_id, double* algo_bytes_out);
 
 #ifdef __cplusplus
 }

@@ -17,13 +17,15 @@ c_int = ctypes.c_int
 
 STOP_FIXED, STOP_REF_COMPAT, STOP_ARGMAX_STABLE, STOP_TOLX = 0, 1, 2, 3
 LABEL_ARGMAX, LABEL_R_ORDER = 0, 1
-KID_WTA, KID_HUPD, KID_AHTW, KID_INIT, KID_LABEL = 0, 1, 2, 3, 4
+INIT_LIBNMF, INIT_R_RUNIF = 0, 1
+KID_WTA, KID_HUPD, KID_AHTW, KID_INIT, KID_OTHER, KID_LABELS, KID_COUNTS = 0, 1, 2, 3, 4, 5, 6
 
 
 class SweepOpts(ctypes.Structure):
     _fields_ = [("maxiter", c_int), ("stop_rule", c_int), ("label_rule", c_int), ("seed", ctypes.c_uint32),
                 ("min_init", c_int), ("max_init", c_int), ("job_begin", c_int), ("job_end", c_int),
-                ("check_every", c_int), ("verbose", c_int), ("TolX", ctypes.c_double), ("TolFun", ctypes.c_double)]
+                ("check_every", c_int), ("verbose", c_int), ("TolX", ctypes.c_double), ("TolFun", ctypes.c_double),
+                ("init_stream", c_int)]
 
 
 class Result(ctypes.Structure):
@@ -55,8 +57,9 @@ EXPORTED = [
     "calculateNorm", "calculateMaxchange",
     # include/nmfc.h
     "nmfc_engine_create", "nmfc_engine_destroy", "nmfc_default_opts", "nmfc_engine_run", "nmfc_sweep",
-    "nmfc_consensus", "nmfc_cophenetic", "nmfc_cutree", "nmfc_last_error", "nmfc_version", "nmfc_engine_kernel_time",
-    "nmfc_engine_set_timing", "nmfc_engine_kernel_flops",
+    "nmfc_consensus", "nmfc_cophenetic", "nmfc_cophenetic_batch", "nmfc_cutree", "nmfc_last_error", "nmfc_version", "nmfc_engine_kernel_time",
+    "nmfc_engine_set_timing", "nmfc_engine_kernel_flops", "nmfc_engine_kernel_bytes",
+    "nmfc_calculate_norm_dev", "nmfc_calculate_maxchange_dev",
     "nmfc_brunet_default_opts", "nmfc_brunet_create", "nmfc_brunet_destroy", "nmfc_brunet_run",
     "nmfc_brunet_set_timing", "nmfc_brunet_kernel_time",
 ]
@@ -111,6 +114,8 @@ def lib() -> ctypes.CDLL:
     L.nmfc_consensus.restype = c_int
     L.nmfc_cophenetic.argtypes = [_dp, c_int, _ip, _ip, _dp]
     L.nmfc_cophenetic.restype = ctypes.c_double
+    L.nmfc_cophenetic_batch.argtypes = [_dp, c_int, c_int, c_int, _dp, _ip, _ip, _dp]
+    L.nmfc_cophenetic_batch.restype = c_int
     L.nmfc_cutree.argtypes = [_ip, c_int, c_int, _ip]
     L.nmfc_cutree.restype = c_int
     L.nmfc_last_error.argtypes = []
@@ -123,6 +128,13 @@ def lib() -> ctypes.CDLL:
     L.nmfc_engine_set_timing.restype = None
     L.nmfc_engine_kernel_flops.argtypes = [ctypes.c_void_p, c_int]
     L.nmfc_engine_kernel_flops.restype = ctypes.c_double
+    L.nmfc_engine_kernel_bytes.argtypes = [ctypes.c_void_p, c_int, _dp]
+    L.nmfc_engine_kernel_bytes.restype = ctypes.c_double
+    vp = ctypes.c_void_p
+    L.nmfc_calculate_norm_dev.argtypes = [vp, vp, vp, vp, c_int, c_int, c_int, _dp, _dp]
+    L.nmfc_calculate_norm_dev.restype = c_int
+    L.nmfc_calculate_maxchange_dev.argtypes = [vp, vp, c_int, c_int, ctypes.c_double, _dp, _dp]
+    L.nmfc_calculate_maxchange_dev.restype = c_int
     L.nmfc_brunet_default_opts.argtypes = [ctypes.POINTER(BrunetOpts)]
     L.nmfc_brunet_default_opts.restype = None
     L.nmfc_brunet_create.argtypes = [c_int, ctypes.c_void_p, c_int, c_int, c_int]

@@ -50,6 +50,7 @@ class BrunetEngine:
             raise RuntimeError(f"nmfc_brunet_create failed: {_lib.last_error()}")
         self.h = h
         self.m, self.n = m, n
+        self.device = device   # HIP device ordinal (-1: the device current at creation)
 
     def close(self):
         if getattr(self, "h", None):

@@ -33,6 +33,7 @@
 #include <thread>
 #include <vector>
 
+#include "rmt.hpp"
 #include "../../include/nmfc.h"
 
 void nmfc_set_error(const char* msg);
@@ -160,53 +161,24 @@ constexpr int rg_small(int K) {
 // Kernels
 // ------------------------------------------------------------------------------------------------
 
-__device__ __forceinline__ uint32_t mt_step(uint32_t cur, uint32_t nxt, uint32_t far) {
-  const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
-  return far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-}
-
 // set.seed(seeds[b]); W <- matrix(runif(m*K), m, K); H <- matrix(runif(K*n), K, n)  (one workgroup per
-// restart).  The 624-word regeneration runs in four dependency phases: kk < 227 reads old words only;
-// 227 <= kk < 454 and 454 <= kk < 623 read kk - 227 from the previous phase; kk = 623 reads 0 and 396.
+// restart; R's Mersenne-Twister from rmt.hpp).
 __global__ __launch_bounds__(BT) void k_br_init(const uint32_t* __restrict__ seeds, int m, int n, int K,
                                                 double* __restrict__ W, long wstride, double* __restrict__ H,
                                                 long hstride) {
   __shared__ uint32_t mt[624];
   const int b = blockIdx.x, tid = threadIdx.x;
-  if (tid == 0) {
-    uint32_t s = seeds[b];
-    for (int j = 0; j < 51; ++j) s = 69069u * s + 1u;   // 50 scrambling steps + the mti slot
-    for (int j = 0; j < 624; ++j) {
-      s = 69069u * s + 1u;
-      mt[j] = s;
-    }
-  }
+  if (tid == 0) rmt::seed_table(mt, seeds[b]);
   __syncthreads();
   const long nw = (long)m * K, total = nw + (long)K * n;
   double* Wb = W + (long)b * wstride;
   double* Hb = H + (long)b * hstride;
-  const int plo[4] = {0, 227, 454, 623}, phi[4] = {227, 454, 623, 624};
   for (long base = 0; base < total; base += 624) {
-    for (int ph = 0; ph < 4; ++ph) {
-      const int kk = plo[ph] + tid;
-      const bool mine = kk < phi[ph];
-      uint32_t v = 0;
-      if (mine) v = mt_step(mt[kk], mt[kk == 623 ? 0 : kk + 1], mt[kk < 227 ? kk + 397 : kk - 227]);
-      __syncthreads();
-      if (mine) mt[kk] = v;
-      __syncthreads();
-    }
+    rmt::regenerate<BT>(mt);
     for (int t = tid; t < 624; t += BT) {
       const long d = base + t;
       if (d >= total) break;
-      uint32_t y = mt[t];
-      y ^= (y >> 11);
-      y ^= (y << 7) & 0x9d2c5680u;
-      y ^= (y << 15) & 0xefc60000u;
-      y ^= (y >> 18);
-      double u = (double)y * 2.3283064365386963e-10;
-      if (u <= 0.0) u = 0.5 * 2.328306437080797e-10;
-      else if (1.0 - u <= 0.0) u = 1.0 - 0.5 * 2.328306437080797e-10;
+      const double u = rmt::unif(mt[t]);
       if (d < nw)
         Wb[(d % m) * K + d / m] = u;
       else

@@ -9,11 +9,16 @@
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/libnmf_compat.h"
 #include "../../include/nmfc.h"
 #include "nmfc_kernels.hpp"
+
+namespace {
+constexpr size_t NORM_BLOCKS = 4096;   // grid of the norm / max-change partial passes (>> 256 CUs)
+}
 
 extern "C" {
 
@@ -144,67 +149,117 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
   return 0;
 }
 
-// calculatenorm.c:44-78 -- d = a - w h and ||d||_F / sqrt(m n), one fused GPU pass + host sum of
-// per-block partials in block order (deterministic).
-double calculateNorm(double* a, double* w, double* h, double* d, int m, int n, int k) {
-  const size_t la = (size_t)m * n, lw = (size_t)m * k, lh = (size_t)k * n;
-  double *da = nullptr, *dw = nullptr, *dh = nullptr, *dd = nullptr, *dp = nullptr;
-  const int blocks = (int)std::min<size_t>((la + nmfc::NT - 1) / nmfc::NT, 1024);
+// calculatenorm.c:44-78 on device operands: d = a - w h and ||d||_F / sqrt(m n), one fused GPU pass +
+// a host sum of the per-block partials in block order (deterministic).  ms_out: device time of the pass.
+int nmfc_calculate_norm_dev(const double* da, const double* dw, const double* dh, double* dd, int m, int n, int k,
+                            double* norm_out, double* ms_out) {
+  if (!da || !dw || !dh || !dd || m <= 0 || n <= 0 || k <= 0 || !norm_out) return -1;
+  const size_t la = (size_t)m * n;
+  const int blocks = (int)std::min<size_t>((la + nmfc::NT - 1) / nmfc::NT, NORM_BLOCKS);
   std::vector<double> part(blocks);
-  double result = NAN;
-  if (hipMalloc(&da, la * 8) || hipMalloc(&dw, lw * 8) || hipMalloc(&dh, lh * 8) || hipMalloc(&dd, la * 8) ||
-      hipMalloc(&dp, blocks * 8))
-    goto done;
-  if (hipMemcpy(da, a, la * 8, hipMemcpyHostToDevice) || hipMemcpy(dw, w, lw * 8, hipMemcpyHostToDevice) ||
-      hipMemcpy(dh, h, lh * 8, hipMemcpyHostToDevice))
-    goto done;
+  double* dp = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int rc = -1;
+  if (hipMalloc(&dp, blocks * 8) != hipSuccess) goto done;
+  if (ms_out && (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess)) goto done;
+  if (ms_out) (void)hipEventRecord(ev[0], 0);
   hipLaunchKernelGGL(nmfc::k_norm_partial, dim3(blocks), dim3(nmfc::NT), 0, 0, da, dw, dh, dd, m, n, k, dp);
   if (hipGetLastError() != hipSuccess) goto done;
-  if (hipMemcpy(d, dd, la * 8, hipMemcpyDeviceToHost) || hipMemcpy(part.data(), dp, blocks * 8, hipMemcpyDeviceToHost))
-    goto done;
+  if (ms_out) (void)hipEventRecord(ev[1], 0);
+  if (hipMemcpy(part.data(), dp, blocks * 8, hipMemcpyDeviceToHost) != hipSuccess) goto done;
   {
     double ss = 0.0;
     for (int b = 0; b < blocks; ++b) ss += part[b];
-    result = sqrt(ss) / sqrt((double)m * n);
+    *norm_out = sqrt(ss) / sqrt((double)m * n);
   }
+  if (ms_out) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+    *ms_out = ms;
+  }
+  rc = 0;
 done:
-  if (std::isnan(result)) fprintf(stderr, "calculateNorm: device failure\n");
-  (void)hipFree(da);
-  (void)hipFree(dw);
-  (void)hipFree(dh);
-  (void)hipFree(dd);
+  for (hipEvent_t x : ev)
+    if (x) (void)hipEventDestroy(x);
   (void)hipFree(dp);
-  return result;
+  return rc;
 }
 
-// calculatemaxchange.c:42-71 -- max|mat0 - mat| / (sqrteps + max|mat0|); mat0 -= mat (exact, order-free)
-double calculateMaxchange(double* mat, double* mat0, int m, int n, const double sqrteps) {
+// calculatemaxchange.c:42-71 on device operands: max|mat0 - mat| / (sqrteps + max|mat0|); mat0 -= mat
+// (exact and order-free).
+int nmfc_calculate_maxchange_dev(const double* dm, double* dm0, int m, int n, double sqrteps, double* out,
+                                 double* ms_out) {
+  if (!dm || !dm0 || m <= 0 || n <= 0 || !out) return -1;
   const size_t len = (size_t)m * n;
-  double *dm = nullptr, *dm0 = nullptr, *dp = nullptr;
-  const int blocks = (int)std::min<size_t>((len + nmfc::NT - 1) / nmfc::NT, 1024);
+  const int blocks = (int)std::min<size_t>((len + nmfc::NT - 1) / nmfc::NT, NORM_BLOCKS);
   std::vector<double> part(2 * blocks);
-  double result = NAN;
-  if (hipMalloc(&dm, len * 8) || hipMalloc(&dm0, len * 8) || hipMalloc(&dp, 2 * blocks * 8)) goto done;
-  if (hipMemcpy(dm, mat, len * 8, hipMemcpyHostToDevice) || hipMemcpy(dm0, mat0, len * 8, hipMemcpyHostToDevice))
-    goto done;
+  double* dp = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int rc = -1;
+  if (hipMalloc(&dp, 2 * blocks * 8) != hipSuccess) goto done;
+  if (ms_out && (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess)) goto done;
+  if (ms_out) (void)hipEventRecord(ev[0], 0);
   hipLaunchKernelGGL(nmfc::k_maxchange_partial, dim3(blocks), dim3(nmfc::NT), 0, 0, dm, dm0, (long)len, dp);
   if (hipGetLastError() != hipSuccess) goto done;
-  if (hipMemcpy(mat0, dm0, len * 8, hipMemcpyDeviceToHost) ||
-      hipMemcpy(part.data(), dp, 2 * blocks * 8, hipMemcpyDeviceToHost))
-    goto done;
+  if (ms_out) (void)hipEventRecord(ev[1], 0);
+  if (hipMemcpy(part.data(), dp, 2 * blocks * 8, hipMemcpyDeviceToHost) != hipSuccess) goto done;
   {
     double mx0 = 0.0, mxd = 0.0;
     for (int b = 0; b < blocks; ++b) {
       mx0 = fmax(mx0, part[2 * b]);
       mxd = fmax(mxd, part[2 * b + 1]);
     }
-    result = mxd / (sqrteps + mx0);
+    *out = mxd / (sqrteps + mx0);
   }
+  if (ms_out) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+    *ms_out = ms;
+  }
+  rc = 0;
+done:
+  for (hipEvent_t x : ev)
+    if (x) (void)hipEventDestroy(x);
+  (void)hipFree(dp);
+  return rc;
+}
+
+// calculatenorm.c:44-78 -- host operands: upload, nmfc_calculate_norm_dev, download d.
+double calculateNorm(double* a, double* w, double* h, double* d, int m, int n, int k) {
+  const size_t la = (size_t)m * n, lw = (size_t)m * k, lh = (size_t)k * n;
+  double *da = nullptr, *dw = nullptr, *dh = nullptr, *dd = nullptr;
+  double result = NAN, v = 0.0;
+  if (hipMalloc(&da, la * 8) || hipMalloc(&dw, lw * 8) || hipMalloc(&dh, lh * 8) || hipMalloc(&dd, la * 8)) goto done;
+  if (hipMemcpy(da, a, la * 8, hipMemcpyHostToDevice) || hipMemcpy(dw, w, lw * 8, hipMemcpyHostToDevice) ||
+      hipMemcpy(dh, h, lh * 8, hipMemcpyHostToDevice))
+    goto done;
+  if (nmfc_calculate_norm_dev(da, dw, dh, dd, m, n, k, &v, nullptr) != 0) goto done;
+  if (hipMemcpy(d, dd, la * 8, hipMemcpyDeviceToHost)) goto done;
+  result = v;
+done:
+  if (std::isnan(result)) fprintf(stderr, "calculateNorm: device failure\n");
+  (void)hipFree(da);
+  (void)hipFree(dw);
+  (void)hipFree(dh);
+  (void)hipFree(dd);
+  return result;
+}
+
+// calculatemaxchange.c:42-71 -- host operands: upload, nmfc_calculate_maxchange_dev, download mat0.
+double calculateMaxchange(double* mat, double* mat0, int m, int n, const double sqrteps) {
+  const size_t len = (size_t)m * n;
+  double *dm = nullptr, *dm0 = nullptr;
+  double result = NAN, v = 0.0;
+  if (hipMalloc(&dm, len * 8) || hipMalloc(&dm0, len * 8)) goto done;
+  if (hipMemcpy(dm, mat, len * 8, hipMemcpyHostToDevice) || hipMemcpy(dm0, mat0, len * 8, hipMemcpyHostToDevice))
+    goto done;
+  if (nmfc_calculate_maxchange_dev(dm, dm0, m, n, sqrteps, &v, nullptr) != 0) goto done;
+  if (hipMemcpy(mat0, dm0, len * 8, hipMemcpyDeviceToHost)) goto done;
+  result = v;
 done:
   if (std::isnan(result)) fprintf(stderr, "calculateMaxchange: device failure\n");
   (void)hipFree(dm);
   (void)hipFree(dm0);
-  (void)hipFree(dp);
   return result;
 }
 

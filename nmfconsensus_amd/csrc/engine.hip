@@ -49,9 +49,14 @@ void set_err(const char* fmt, ...) {
 
 long round_up(long v, long a) { return (v + a - 1) / a * a; }
 
+// Device buffer, released on destruction (every early return frees what it allocated).
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   int ensure(size_t need) {
     if (need <= bytes) return 0;
     if (p) (void)hipFree(p);
@@ -110,7 +115,7 @@ std::vector<uint32_t> make_jump_table(int nchunks) {
   return table;
 }
 
-enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID_N = 5 };
+enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID_LABELS = 5, KID_COUNTS = 6, KID_N = 7 };
 
 // Packing of a restart list into 64-column panels by first-fit decreasing (k descending, ties by rid;
 // a restart never straddles a panel), so the k = 10 / 6 / 5 panels' spare columns take small-k
@@ -199,6 +204,8 @@ struct nmfc_engine {
   double kms[KID_N] = {0};
   long long kcount[KID_N] = {0};
   double kflops[KID_N] = {0};
+  double kbytes[KID_N] = {0};       // bytes the kernel's design moves per launch (operands + partials)
+  double kbytes_algo[KID_N] = {0};  // algorithmic bytes per launch (each operand once)
   int repacks = 0;
 };
 
@@ -373,6 +380,12 @@ double nmfc_engine_kernel_flops(nmfc_engine* e, int kid) {
   return e->kflops[kid];
 }
 
+double nmfc_engine_kernel_bytes(nmfc_engine* e, int kid, double* algo_bytes_out) {
+  if (!e || kid < 0 || kid >= KID_N) return 0.0;
+  if (algo_bytes_out) *algo_bytes_out = e->kbytes_algo[kid];
+  return e->kbytes[kid];
+}
+
 int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_sweep_opts* opts_in,
                     const double* W_init, const double* H_init, nmfc_result* out) {
   if (!e || !ks || nk <= 0 || R <= 0) {
@@ -397,8 +410,9 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     set_err("nmfc_engine_run: maxiter must be >= 0");
     return -1;
   }
-  if (opts.stop_rule < 0 || opts.stop_rule > 3 || opts.label_rule < 0 || opts.label_rule > 1) {
-    set_err("nmfc_engine_run: bad stop or label rule");
+  if (opts.stop_rule < 0 || opts.stop_rule > 3 || opts.label_rule < 0 || opts.label_rule > 1 ||
+      opts.init_stream < 0 || opts.init_stream > 1) {
+    set_err("nmfc_engine_run: bad stop rule, label rule or init stream");
     return -1;
   }
   HCHECK(hipSetDevice(e->dev));
@@ -407,6 +421,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     e->kms[q] = 0;
     e->kcount[q] = 0;
     e->kflops[q] = 0;
+    e->kbytes[q] = 0;
+    e->kbytes_algo[q] = 0;
   }
   e->repacks = 0;
   const long njobs_all = (long)nk * R;
@@ -506,6 +522,22 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                               sizeof(double) * n, sizeof(double) * n, k, hipMemcpyHostToDevice, st));
       HCHECK(hipStreamSynchronize(st));   // hrow is reused
     }
+  } else if (opts.init_stream == NMFC_INIT_R_RUNIF) {
+    // nmf.r:37-38 under the BatchJobs job seed (seed + job_id - 1)
+    std::vector<InitJob> ij(nj);
+    for (int q = 0; q < nj; ++q) {
+      const RestartInfo& r = pk.ri[q];
+      ij[q] = InitJob{(uint32_t)(opts.seed + (uint32_t)(jb + rslot[r.rid])), r.col0, r.k, 0};
+    }
+    if (e->initjobs.ensure(sizeof(InitJob) * nj)) return -1;
+    HCHECK(hipMemcpyAsync(e->initjobs.p, ij.data(), sizeof(InitJob) * nj, hipMemcpyHostToDevice, st));
+    {
+      TimedLaunch tl(e, KID_INIT);
+      hipLaunchKernelGGL(k_init_runif, dim3(nj), dim3(NT), 0, st, e->initjobs.as<InitJob>(), m, n, e->m_pad, e->n_pad,
+                         e->W[0].as<double>(), e->H[0].as<double>());
+    }
+    HCHECK(hipGetLastError());
+    HCHECK(hipStreamSynchronize(st));   // ij goes out of scope
   } else {
     std::vector<InitJob> ij(nj);
     std::vector<int> cj, ci;
@@ -573,7 +605,14 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   int it = 0, q = 0, checked = 0;
   int nact = nj;
   int stopped_at_pack = 0;
-  hipEvent_t ev[2];
+  struct PollEvents {   // destroyed on every exit path, including HCHECK returns
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    ~PollEvents() {
+      for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } pe;
+  hipEvent_t* ev = pe.ev;
   HCHECK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
   HCHECK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
   std::vector<int> si(nj);
@@ -691,6 +730,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       for (const RestartInfo& r : pk.ri) (si[r.rid] ? gone : live).push_back(r);
       if (archive(gone)) return -1;
       Packing np = pack(live);
+      if ((long)np.npanels * PANEL > cap_cols) {
+        // first-fit decreasing is not monotone under removal: a (rare) larger packing would overrun
+        // the buffers sized from the initial one, so keep the current placement until the next poll
+        stopped_at_pack = stopped;
+        continue;
+      }
       std::vector<int> old_col(nj, -1);
       for (const RestartInfo& r : live) old_col[r.rid] = r.col0;
       std::vector<MoveJob> mv(np.ri.size());
@@ -718,8 +763,6 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   }
   HCHECK(hipStreamSynchronize(st));
   if (e->timing) drain_timing(e);
-  (void)hipEventDestroy(ev[0]);
-  (void)hipEventDestroy(ev[1]);
   const int iters_enqueued = it;
   auto t_iter1 = std::chrono::steady_clock::now();
   {
@@ -734,7 +777,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   for (int rid = 0; rid < nj; ++rid) fin[rid] = {hoff[rid], all[rid].k, rid, all[rid].sq_off};
   HCHECK(hipMemcpyAsync(e->finfo.p, fin.data(), sizeof(RestartInfo) * nj, hipMemcpyHostToDevice, st));
   {
-    TimedLaunch tl(e, KID_OTHER);
+    TimedLaunch tl(e, KID_LABELS);
     hipLaunchKernelGGL(k_labels, dim3((n + NT - 1) / NT, nj), dim3(NT), 0, st, e->finfo.as<RestartInfo>(),
                        e->slot.as<int>(), e->Hfin.as<double>(), e->n_pad, n, opts.label_rule, e->labels.as<int32_t>());
   }
@@ -760,7 +803,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       dcounts = e->counts_tmp.as<int32_t>();
     }
     {
-      TimedLaunch tl(e, KID_OTHER);
+      TimedLaunch tl(e, KID_COUNTS);
       hipLaunchKernelGGL(k_counts, dim3((n + 15) / 16, (n + 15) / 16, nk), dim3(NT), 0, st, e->labels.as<int32_t>(),
                          e->grp_begin.as<int>(), e->grp_list.as<int>(), n, dcounts);
     }
@@ -786,6 +829,9 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   long long tot_iters = 0;
   int max_it = 0;
   double fl_wta = 0, fl_ahtw = 0;
+  // bytes, summed over restart-iterations (each restart takes part in `itr` launches of each MU kernel)
+  double b_wta = 0, ba_wta = 0, b_ahtw = 0, ba_ahtw = 0, b_hupd = 0, ba_hupd = 0, b_lab = 0, cols = 0;
+  const double ns = e->nsplit;
   for (int rid = 0; rid < nj; ++rid) {
     const int itr = si[rid] ? si[rid] : iters_enqueued;
     tot_iters += itr;
@@ -794,11 +840,41 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     // algorithmic flops (nmf_mu.c:174-202 at 2*M*N*K each): W^T A + W^T W  |  A h^T + W0 (h h^T)
     fl_wta += (double)itr * (2.0 * m * n * k + 2.0 * m * k * k);
     fl_ahtw += (double)itr * (2.0 * m * n * k + 2.0 * m * k * k);
+    // W^T A: W read + G written (algorithmic) | + the split-K partials and Gram partials (design)
+    ba_wta += itr * 8.0 * k * (m + n);
+    b_wta += itr * 8.0 * k * (m + ns * n + ns * k);
+    // A h^T + W update: h, W0 read, W written
+    ba_ahtw += itr * 8.0 * k * (2.0 * m + n);
+    b_ahtw += itr * 8.0 * k * (2.0 * m + n + KMAX);
+    // H update (SURVEY 8(d) B_ew, H side): H, numerator, denominator read, H written = 32 n k
+    ba_hupd += itr * 32.0 * n * k;
+    b_hupd += itr * 8.0 * (k * n * (ns + 2.0) + k * k * (ns + 2.0) + k * KMAX);
+    b_lab += 8.0 * k * n + 4.0 * n;
+    cols += k;
     if (out && out->iters) out->iters[rslot[rid]] = itr;
     if (out && out->stopped_early) out->stopped_early[rslot[rid]] = (sr[rid] == 1 || sr[rid] == 3);
   }
-  if (e->kcount[KID_WTA]) e->kflops[KID_WTA] = fl_wta / e->kcount[KID_WTA];
-  if (e->kcount[KID_AHTW]) e->kflops[KID_AHTW] = fl_ahtw / e->kcount[KID_AHTW];
+  const double a_bytes = 8.0 * m * n;   // A, read once per launch by each contraction
+  if (const long long c = e->kcount[KID_WTA]) {
+    e->kflops[KID_WTA] = fl_wta / c;
+    e->kbytes_algo[KID_WTA] = a_bytes + ba_wta / c;
+    e->kbytes[KID_WTA] = a_bytes + b_wta / c;
+  }
+  if (const long long c = e->kcount[KID_AHTW]) {
+    e->kflops[KID_AHTW] = fl_ahtw / c;
+    e->kbytes_algo[KID_AHTW] = a_bytes + ba_ahtw / c;
+    e->kbytes[KID_AHTW] = a_bytes + b_ahtw / c;
+  }
+  if (const long long c = e->kcount[KID_HUPD]) {
+    e->kbytes_algo[KID_HUPD] = ba_hupd / c;
+    e->kbytes[KID_HUPD] = b_hupd / c;
+  }
+  if (e->kcount[KID_LABELS]) e->kbytes[KID_LABELS] = e->kbytes_algo[KID_LABELS] = b_lab;   // one launch
+  if (e->kcount[KID_COUNTS]) {   // labels of each k group read once, n x n int32 counts written per k
+    e->kbytes_algo[KID_COUNTS] = 4.0 * nj * n + 4.0 * nk * n * n;
+    e->kbytes[KID_COUNTS] = e->kbytes_algo[KID_COUNTS];
+  }
+  (void)cols;
 
   if (out && (out->W || out->H)) {
     std::vector<long> woff(nj + 1, 0), ho(nj + 1, 0);

@@ -8,8 +8,11 @@
 //   * the merge/order post-processing of R's hcass2,
 //   * cophenetic heights from the merge sequence, Pearson correlation with long-double sums.
 // n <= a few thousand (consensus matrices are n x n), so O(n^2) memory and time are fine here.
+#include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <thread>
 #include <vector>
 
 #include "../../include/nmfc.h"
@@ -225,6 +228,26 @@ double nmfc_cophenetic(const double* C, int n, int32_t* order_out, int32_t* merg
   }
   if (sxx <= 0 || syy <= 0) return NAN;
   return (double)(sxy / (sqrtl(sxx) * sqrtl(syy)));
+}
+
+int nmfc_cophenetic_batch(const double* C, int nk, int n, int nthreads, double* rho_out, int32_t* order_out,
+                          int32_t* merge_out, double* height_out) {
+  if (!C || nk < 1 || n < 2 || !rho_out) return -1;
+  if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+  nthreads = std::min(nthreads, nk);
+  const long nn = (long)n * n;
+  std::atomic<int> next(0);
+  auto work = [&] {
+    for (int q; (q = next.fetch_add(1)) < nk;)
+      rho_out[q] = nmfc_cophenetic(C + q * nn, n, order_out ? order_out + (long)q * n : nullptr,
+                                   merge_out ? merge_out + (long)q * 2 * (n - 1) : nullptr,
+                                   height_out ? height_out + (long)q * (n - 1) : nullptr);
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nthreads; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  return 0;
 }
 
 int nmfc_cutree(const int32_t* merge, int n, int k, int32_t* membership_out) {

@@ -31,19 +31,37 @@ def allreduce_counts(counts, group=None):
     return counts
 
 
+def _engine_device(engine):
+    import torch
+
+    dev = getattr(engine, "device", -1)
+    return torch.device("cuda", dev if dev is not None and dev >= 0 else torch.cuda.current_device())
+
+
+def _counts_for(engine, nk, n, counts_tensor):
+    """The (nk, n, n) int32 count tensor on the engine's GPU.  The engine writes it on its own stream, so
+    torch's stream is drained first: nothing torch queued on the tensor (a zero fill, the previous
+    all-reduce) may still be running when the engine starts writing."""
+    import torch
+
+    if counts_tensor is None:
+        counts_tensor = torch.zeros((nk, n, n), dtype=torch.int32, device=_engine_device(engine))
+    if counts_tensor.is_cuda:
+        torch.cuda.current_stream(counts_tensor.device).synchronize()
+    return counts_tensor
+
+
 def run_sharded_sweep(engine, ks, R: int, *, rank: int, world: int, counts_tensor=None, group=None, reduce: bool = True,
                       **run_kwargs):
     """Runs this rank's shard on `engine` (nmfconsensus_amd.nmf.Engine on the rank's GPU) and
     all-reduces the counts.  `counts_tensor`: a torch.int32 CUDA tensor of shape (nk, n, n) that the
-    engine writes directly (device pointer) and RCCL reduces; allocated if None.
-    Returns (counts_tensor_after_allreduce, local SweepResult)."""
-    import torch
-
+    engine writes directly (device pointer) and RCCL reduces; allocated on the engine's device if None.
+    The engine's run returns after its stream has finished writing the counts, so the all-reduce
+    (queued on torch's stream) reads complete data.  Returns (counts_tensor_after_allreduce, local SweepResult)."""
     nk = len(ks)
     n = engine.n
     jb, je = shard_range(nk * R, rank, world)
-    if counts_tensor is None:
-        counts_tensor = torch.zeros((nk, n, n), dtype=torch.int32, device="cuda")
+    counts_tensor = _counts_for(engine, nk, n, counts_tensor)
     res = engine.run(ks, R, job_begin=jb, job_end=je, counts_device_ptr=counts_tensor.data_ptr(), **run_kwargs)
     if world > 1 and reduce:
         allreduce_counts(counts_tensor, group)
@@ -71,13 +89,10 @@ def run_sharded_brunet(engine, ks, R: int, *, rank: int, world: int, counts_tens
                        reduce: bool = True, **run_kwargs):
     """Runs this rank's restart shard on `engine` (nmfconsensus_amd.brunet.BrunetEngine) and
     all-reduces the int32 counts (RCCL on GPUs).  Returns (counts_tensor, local SweepResult)."""
-    import torch
-
     nk = len(ks)
     n = engine.n
     rb, re = shard_range(R, rank, world)
-    if counts_tensor is None:
-        counts_tensor = torch.zeros((nk, n, n), dtype=torch.int32, device="cuda")
+    counts_tensor = _counts_for(engine, nk, n, counts_tensor)
     res = engine.run(ks, R, restart_begin=rb, restart_end=re, counts_device_ptr=counts_tensor.data_ptr(), **run_kwargs)
     if world > 1 and reduce:
         allreduce_counts(counts_tensor, group)

@@ -12,8 +12,9 @@ workflow reads the same:
 
 Every compute step calls nmfconsensus_amd/libnmf.so (HIP, gfx950); there is no CPU fallback.
 Differences from nmf.r, all documented in DESIGN.md:
-  * per-job init uses libnmf's generateMatrix(ran) stream (glibc rand, job seed = seed + job_id - 1)
-    instead of R's runif under BatchJobs seeds (north star; R is absent from the image);
+  * per-job init defaults to libnmf's generateMatrix(ran) stream (glibc rand, job seed = seed + job_id - 1,
+    the north star's choice); init_stream=INIT_R_RUNIF gives nmf.r:37-38's runif under the BatchJobs job
+    seed (R's Mersenne-Twister restated, bit-exact; BatchJobs' seed rule itself is unpinned);
   * the consensus is built from the FINAL H of every restart (what nmf.r intends; with R >= 3.2 the
     literal nmf.r:47-50 returns the initial H, see SURVEY.md 0.5);
   * label_rule selects nmf.r:128's literal `order()[1]` (argmin, LABEL_R_ORDER) or the documented
@@ -28,13 +29,14 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import (LABEL_ARGMAX, LABEL_R_ORDER, STOP_ARGMAX_STABLE, STOP_FIXED, STOP_REF_COMPAT, STOP_TOLX, Result,
+from ._lib import (INIT_LIBNMF, INIT_R_RUNIF, LABEL_ARGMAX, LABEL_R_ORDER, STOP_ARGMAX_STABLE, STOP_FIXED, STOP_REF_COMPAT, STOP_TOLX, Result,
                    SweepOpts)
 
 __all__ = [
     "Engine", "SweepResult", "doNMF", "createJobArray", "runNMFinJobs", "computeConsensusMatrixFromClusterings",
-    "computeConsensusAndSaveFiles", "cophenetic", "cutree", "job_grid",
+    "computeConsensusAndSaveFiles", "cophenetic", "cophenetic_batch", "cutree", "job_grid",
     "STOP_FIXED", "STOP_REF_COMPAT", "STOP_ARGMAX_STABLE", "STOP_TOLX", "LABEL_ARGMAX", "LABEL_R_ORDER",
+    "INIT_LIBNMF", "INIT_R_RUNIF",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -99,6 +101,7 @@ class Engine:
             raise RuntimeError(f"nmfc_engine_create failed: {_lib.last_error()}")
         self.h = h
         self.m, self.n = m, n
+        self.device = device   # HIP device ordinal (-1: the device current at creation)
 
     def close(self):
         if getattr(self, "h", None):
@@ -128,11 +131,17 @@ class Engine:
     def kernel_flops(self, kid: int) -> float:
         return self.L.nmfc_engine_kernel_flops(self.h, kid)
 
+    def kernel_bytes(self, kid: int):
+        """(design bytes, algorithmic bytes) per launch of kernel `kid` in the last run."""
+        algo = ctypes.c_double(0.0)
+        b = self.L.nmfc_engine_kernel_bytes(self.h, kid, ctypes.byref(algo))
+        return b, algo.value
+
     def run(self, ks, R: int, *, maxiter: int = 10000, seed: int = 123, stop_rule: int = STOP_REF_COMPAT,
             label_rule: int = LABEL_ARGMAX, job_begin: int = 0, job_end: int = -1, W_init=None, H_init=None,
             want_factors: bool = False, want_counts: bool = True, counts_device_ptr: int | None = None,
             check_every: int = 16, min_init: int = 0, max_init: int = 1, verbose: bool = False,
-            TolX: float = 1e-4, TolFun: float = 1e-4) -> SweepResult:
+            TolX: float = 1e-4, TolFun: float = 1e-4, init_stream: int = INIT_LIBNMF) -> SweepResult:
         ks = [int(k) for k in ks]
         nk = len(ks)
         njobs_all = nk * R
@@ -148,6 +157,7 @@ class Engine:
         o.job_begin, o.job_end, o.check_every, o.verbose = jb, je, check_every, 1 if verbose else 0
         o.min_init, o.max_init = min_init, max_init
         o.TolX, o.TolFun = TolX, TolFun
+        o.init_stream = init_stream
         m, n = self.m, self.n
         res = Result()
         iters = np.zeros(nj, dtype=np.int32)
@@ -201,7 +211,7 @@ class Engine:
 
 
 def doNMF(A, k: int, maxniter: int, seed: int = 123, tolerance: float = 1e-4, num_clusterings=None,
-          *, job_id: int = 1, stop_rule: int = STOP_REF_COMPAT):
+          *, job_id: int = 1, stop_rule: int = STOP_REF_COMPAT, init_stream: int = INIT_LIBNMF):
     """nmf.r:23-51 -- one restart: init W, H (generateMatrix(ran) stream, seed + job_id - 1), run the
     MU loop on the GPU, return dict(W=m x k, H=k x n, iter=iterations).  `tolerance` is accepted and
     unused, like the reference (nmf_mu.c:92-93)."""
@@ -209,7 +219,7 @@ def doNMF(A, k: int, maxniter: int, seed: int = 123, tolerance: float = 1e-4, nu
     with Engine(A) as eng:
         # a single-job "grid" whose job seed is seed + job_id - 1
         r = eng.run([k], 1, maxiter=maxniter, seed=seed + job_id - 1, stop_rule=stop_rule, want_factors=True,
-                    want_counts=False)
+                    want_counts=False, init_stream=init_stream)
     return {"W": r.W[0], "H": r.H[0], "iter": int(r.iters[0])}
 
 
@@ -235,7 +245,7 @@ def createJobArray(A, k, num_clusterings: int, maxniter: int, seed: int, toleran
 
 def runNMFinJobs(A, k, num_clusterings: int, maxniter: int, seed: int, njobs: int = 1, *,
                  stop_rule: int = STOP_REF_COMPAT, label_rule: int = LABEL_ARGMAX, save_dir: str | None = None,
-                 device: int = -1):
+                 device: int = -1, init_stream: int = INIT_LIBNMF):
     """nmf.r:106-119: run every (k, restart) job, reduce per k to a consensus matrix, then cophenetic,
     ordering and membership (computeConsensusAndSaveFiles).  `njobs` (BatchJobs chunks) has no effect:
     all jobs run as one batched sweep on the GPU (use nmfconsensus_amd.distributed for several GPUs).
@@ -246,7 +256,8 @@ def runNMFinJobs(A, k, num_clusterings: int, maxniter: int, seed: int, njobs: in
         raise ValueError("Need at least two clusters to compute standard deviation")   # nmf.r:107-108
     reg = createJobArray(A, ks, num_clusterings, maxniter, seed)
     with Engine(reg.A, device) as eng:
-        sw = eng.run(ks, num_clusterings, maxiter=maxniter, seed=seed, stop_rule=stop_rule, label_rule=label_rule)
+        sw = eng.run(ks, num_clusterings, maxiter=maxniter, seed=seed, stop_rule=stop_rule, label_rule=label_rule,
+                     init_stream=init_stream)
     result = {str(kk): sw.consensus[i] for i, kk in enumerate(ks)}
     out = computeConsensusAndSaveFiles(result, save_dir=save_dir)
     out["sweep"] = sw
@@ -281,6 +292,24 @@ def cophenetic(C: np.ndarray):
     return rho, order, merge, height
 
 
+def cophenetic_batch(Cs: np.ndarray, nthreads: int = 0):
+    """cophenetic() for a stack of consensus matrices (nk, n, n), the k's on parallel host threads.
+    Returns (rho[nk], order[nk, n] 1-based, merge[nk, n-1, 2], height[nk, n-1])."""
+    Cs = np.asarray(Cs, dtype=np.float64)
+    nk, n, _ = Cs.shape
+    flat = np.ascontiguousarray(np.transpose(Cs, (0, 2, 1)))   # each matrix column-major
+    rho = np.zeros(nk, dtype=np.float64)
+    order = np.zeros((nk, n), dtype=np.int32)
+    merge = np.zeros((nk, n - 1, 2), dtype=np.int32)
+    height = np.zeros((nk, n - 1), dtype=np.float64)
+    rc = _lib.lib().nmfc_cophenetic_batch(flat.ctypes.data_as(_dp), nk, n, nthreads, rho.ctypes.data_as(_dp),
+                                          order.ctypes.data_as(_ip), merge.ctypes.data_as(_ip),
+                                          height.ctypes.data_as(_dp))
+    if rc != 0:
+        raise ValueError("cophenetic_batch: bad arguments")
+    return rho, order, merge, height
+
+
 def cutree(merge: np.ndarray, k: int) -> np.ndarray:
     """cutree(HC, k) (nmf.r:177): 1-based memberships numbered by first appearance."""
     merge = np.ascontiguousarray(merge, dtype=np.int32)
@@ -304,13 +333,15 @@ def computeConsensusAndSaveFiles(resultList: dict, save_dir: str | None = None, 
 
     k_vec = list(resultList.keys())
     rho, ordered, membership, orders = {}, {}, {}, {}
-    for kk in k_vec:
-        C = np.asarray(resultList[kk])
-        r, order, merge, _ = cophenetic(C)
-        rho[kk] = _signif(r, 4)
+    Cs = np.stack([np.asarray(resultList[kk], dtype=np.float64) for kk in k_vec])
+    rhos, order_all, merge_all, _ = cophenetic_batch(Cs)   # the k's on parallel host threads
+    for q, kk in enumerate(k_vec):
+        C = Cs[q]
+        order = order_all[q]
+        rho[kk] = _signif(float(rhos[q]), 4)
         o = order - 1
         ordered[kk] = C[np.ix_(o, o)]
-        membership[kk] = cutree(merge, int(kk))
+        membership[kk] = cutree(merge_all[q], int(kk))
         orders[kk] = order
     if save_dir:
         os.makedirs(save_dir, exist_ok=True)

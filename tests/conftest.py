@@ -31,3 +31,12 @@ def relfro(a, b):
     a = np.asarray(a)
     b = np.asarray(b)
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+GOLDEN_C2 = os.path.join(ROOT, "tests", "golden", "golden_c2.npz")
+
+
+@pytest.fixture(scope="session")
+def golden_c2():
+    with np.load(GOLDEN_C2, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}

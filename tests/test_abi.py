@@ -60,7 +60,17 @@ def test_set_default_opts_and_check_arguments():
     assert (o.nndsvd_maxiter, o.nndsvd_blocksize, o.nndsvd_tol, o.nndsvd_ncv) == (-1, 64, 2e-16, -1)
     assert libnmf.checkArguments(b"a.matrix", 3, 100, None, None, o) == 0
     assert libnmf.checkArguments(None, 3, 100, None, None, o) == 1
-    assert ctypes.get_errno() in (0, errno.EDOM) or True
+    # checkarguments.c:61-65 sets errno = EDOM: read it through a use_errno handle of the same library
+    from nmfconsensus_amd import _lib
+    Le = ctypes.CDLL(_lib.LIB_PATH, use_errno=True)
+    Le.checkArguments.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
+                                  ctypes.POINTER(_lib.OptionsT)]
+    ctypes.set_errno(0)
+    assert Le.checkArguments(None, 3, 100, None, None, ctypes.byref(o)) == 1
+    assert ctypes.get_errno() == errno.EDOM
+    ctypes.set_errno(0)
+    assert Le.checkArguments(b"a.matrix", 3, 100, None, None, ctypes.byref(o)) == 0
+    assert ctypes.get_errno() == 0
     o.TolX = -1.0
     assert libnmf.checkArguments(b"a.matrix", 3, 100, None, None, o) == 1
 
@@ -120,3 +130,20 @@ def test_cutree_numbering():
     assert list(cutree(merge, 2)) == [1, 1, 2, 2]
     assert list(cutree(merge, 4)) == [1, 2, 3, 4]
     assert list(cutree(merge, 1)) == [1, 1, 1, 1]
+
+
+def test_cophenetic_batch_equals_single():
+    from nmfconsensus_amd.nmf import cophenetic, cophenetic_batch
+    rng = np.random.default_rng(3)
+    n, nk = 61, 5
+    Cs = []
+    for q in range(nk):
+        lab = rng.integers(0, q + 2, size=(20, n))
+        C = np.mean(lab[:, :, None] == lab[:, None, :], axis=0)   # quantised to 1/20: many ties
+        Cs.append(C)
+    Cs = np.array(Cs)
+    rho, order, merge, height = cophenetic_batch(Cs, nthreads=3)
+    for q in range(nk):
+        r1, o1, m1, h1 = cophenetic(Cs[q])
+        assert rho[q] == r1 and np.array_equal(order[q], o1) and np.array_equal(merge[q], m1)
+        assert np.array_equal(height[q], h1)

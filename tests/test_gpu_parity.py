@@ -253,3 +253,53 @@ def test_full_size_c4_shape_vs_oracle(oracle):
     W0, H0 = oracle.init_restart(77 + 13, m, n, 15)
     Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, T, 0)
     assert relfro(r.W[13], Wo) < TOL and relfro(r.H[13], Ho) < TOL
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 40, 2), (1000, 40, 5), (1000, 40, 8), (3001, 150, 16), (97, 33, 3)])
+def test_r_runif_init_bitexact(oracle, golden, m, n, k):
+    """init_stream = R_RUNIF (nmf.r:37-38): set.seed(job seed); W <- runif(m*k); H <- runif(k*n), bit-exact
+    against the R Mersenne-Twister restatement (pinned to R's published values, test_brunet_oracle.py)."""
+    from nmfconsensus_amd.nmf import Engine, INIT_R_RUNIF
+    A = golden["A_gct"] if (m, n) == (1000, 40) else np.asfortranarray(np.random.default_rng(m).random((m, n)))
+    with Engine(A) as eng:
+        r = eng.run([k, 2], 2, maxiter=0, seed=321, init_stream=INIT_R_RUNIF, want_factors=True, want_counts=False)
+    for j, kk in enumerate([k, 2, k, 2]):
+        W, H = oracle.brunet_init(321 + j, m, n, kk)   # job seed = seed + job_id - 1
+        assert np.array_equal(r.W[j], W) and np.array_equal(r.H[j], H), j
+
+
+@pytest.mark.parametrize("rule,key", [(0, "argmax"), (1, "rorder")])
+def test_c1_runif_sweep_vs_reference(gct_engine, golden_c2, rule, key):
+    """The C1 sweep under the R-path init against the reference's own nmf_mu run job by job
+    (tests/golden/make_golden_c2.py): exits, labels, counts bit-exact; H within 1e-9."""
+    from nmfconsensus_amd.nmf import INIT_R_RUNIF
+    g = golden_c2
+    ks = [int(k) for k in g["c1r_ks"]]
+    R = int(g["c1r_R"])
+    r = gct_engine.run(ks, R, maxiter=10000, seed=int(g["c1r_seed"]), stop_rule=1, label_rule=rule,
+                       init_stream=INIT_R_RUNIF, want_factors=True)
+    assert np.array_equal(r.iters, g["c1r_iters"])
+    assert np.array_equal(r.labels, g[f"c1r_labels_{key}"])
+    for i, k in enumerate(ks):
+        assert np.array_equal(r.counts[i], g[f"c1r_counts_{key}_k{k}"])
+        for q, j in enumerate(g[f"c1r_Hjobs_k{k}"]):
+            assert relfro(r.H[j], g[f"c1r_H_k{k}"][q]) < TOL
+
+
+@pytest.mark.parametrize("rule,key", [(0, "argmax"), (1, "rorder")])
+def test_c2_sweep_vs_reference(golden_c2, rule, key):
+    """BASELINE configs[1] (C2): synthetic 1000 x 40, k = 2..8, R = 100 (700 jobs) in one sweep against the
+    reference's own nmf_mu run job by job: exits, labels, counts and consensus bit-exact; H within 1e-9."""
+    from nmfconsensus_amd.nmf import Engine
+    g = golden_c2
+    ks = [int(k) for k in g["c2_ks"]]
+    R = int(g["c2_R"])
+    with Engine(g["c2_A"]) as eng:
+        r = eng.run(ks, R, maxiter=10000, seed=int(g["c2_seed"]), stop_rule=1, label_rule=rule, want_factors=True)
+    assert np.array_equal(r.iters, g["c2_iters"])
+    assert np.array_equal(r.labels, g[f"c2_labels_{key}"])
+    for i, k in enumerate(ks):
+        assert np.array_equal(r.counts[i], g[f"c2_counts_{key}_k{k}"])
+        assert np.array_equal(r.consensus[i], g[f"c2_counts_{key}_k{k}"] / R)
+        for q, j in enumerate(g[f"c2_Hjobs_k{k}"]):
+            assert relfro(r.H[j], g[f"c2_H_k{k}"][q]) < TOL

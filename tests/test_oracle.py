@@ -107,3 +107,25 @@ def test_tolx_rule_oracle(oracle, golden):
     dw = np.max(np.abs(Wp - W)) / (sq + np.max(np.abs(Wp)))
     dh = np.max(np.abs(Hp - H)) / (sq + np.max(np.abs(Hp)))
     assert max(dw, dh) < 1e-3
+
+
+@pytest.mark.parametrize("tag", ["c2", "c1r"])
+def test_c2_and_runif_sweeps_subset(golden, golden_c2, oracle, tag):
+    """The restatement against the reference's own nmf_mu on BASELINE configs[1] (C2, libnmf init) and on
+    the C1 sweep under nmf.r:37-38's runif init (tests/golden/make_golden_c2.py): the first 2 jobs of
+    every k -- exits, labels and H."""
+    g = golden_c2
+    A = g["c2_A"] if tag == "c2" else golden["A_gct"]
+    A = np.asfortranarray(A)
+    m, n = A.shape
+    ks = [int(k) for k in g[f"{tag}_ks"]]
+    seed = int(g[f"{tag}_seed"])
+    for k in ks:
+        for q, j in enumerate(g[f"{tag}_Hjobs_k{k}"]):
+            s = seed + int(j)
+            W0, H0 = oracle.init_restart(s, m, n, k) if tag == "c2" else oracle.brunet_init(s, m, n, k)
+            W, H, it = oracle.nmf_mu(A, W0, H0, 10000, 1)
+            assert it == int(g[f"{tag}_iters"][j]), (k, j)
+            assert np.array_equal(oracle.labels(H, 0), g[f"{tag}_labels_argmax"][j])
+            assert np.array_equal(oracle.labels(H, 1), g[f"{tag}_labels_rorder"][j])
+            assert relfro(H, g[f"{tag}_H_k{k}"][q]) < TOL

@@ -9,7 +9,7 @@
 #include <cmath>
 #include <vector>
 
-#include "../nmfconsensus_amd/csrc/nmfc_kernels.hpp"
+#include "legacy_kernels.hpp"
 
 using namespace nmfc;
 #define CK(x)                                                                     \

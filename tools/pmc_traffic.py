@@ -36,4 +36,8 @@ for kn, d in out.items():
     d["hbm_bytes_per_launch"] = d.get("FETCH_SIZE_bytes_per_launch", 0.0) + d.get("WRITE_SIZE_bytes_per_launch", 0.0)
     d["hbm_bytes_per_full_launch"] = (d.get("FETCH_SIZE_bytes_per_full_launch", 0.0) +
                                       d.get("WRITE_SIZE_bytes_per_full_launch", 0.0))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nmfconsensus_amd.build import source_sha256  # noqa: E402
+
+out["source_sha256"] = source_sha256()   # bench.py uses this profile only for the same kernel source
 print(json.dumps(out, indent=1))
