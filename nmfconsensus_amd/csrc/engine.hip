@@ -172,6 +172,14 @@ Packing pack(const std::vector<RestartInfo>& in) {
   return pk;
 }
 
+// panels holding at least one restart (the packing fills panels from 0; the rest pad the 4-panel groups)
+int live_panels(const Packing& pk) {
+  int np = 0;
+  for (int p = 0; p < pk.npanels; ++p)
+    if (pk.pre[p] > pk.prb[p]) np = p + 1;
+  return np;
+}
+
 }  // namespace
 
 // error slot shared with the other translation units of the library (brunet.hip)
@@ -210,6 +218,47 @@ struct nmfc_engine {
 };
 
 namespace {
+
+// Tile shapes for one chunk of iterations, from a wave-quantised cost model: a shape's time is
+// ceil(workgroups / resident slots) x its relative per-workgroup time.  Slots per CU and relative
+// per-workgroup times (2048-gene chunk, 128 samples of W^T A) were measured on MI355X with
+// tools/tailbench.hip over 1..172 live panels of the C3 shape (profiles/r02/tailbench_*.txt):
+//   big  4 panels x 128 samples, 8 waves, 144 KiB   1 / CU   2.0
+//   mid  2 panels x 128 samples, 8 waves,  96 KiB   1 / CU   1.0
+//   small 1 panel x  64 samples, 4 waves,  48 KiB   3 / CU   0.8
+//   tiny 1 panel x  32 samples, 4 waves,  36 KiB   4 / CU   0.6
+// Ties go to the larger tile.  A h^T uses 64-gene tiles only when the live panels' 128-gene tiles
+// would leave CUs idle.  Every shape accumulates in the canonical K order, so this never changes a bit.
+struct TileChoice {
+  int wta;          // 0 big, 3 mid, 1 small, 2 tiny
+  bool ahtw_small;  // 64-gene A h^T tiles
+};
+
+TileChoice choose_tiles(const nmfc_engine* e, int np_live, int ntj) {
+  const long ns = e->nsplit, cu = e->ncu;
+  const long np = std::max(np_live, 1);
+  struct Cand {
+    int id;
+    long wgs, slots;
+    double t;
+  } cands[4] = {{0, ns * ((np + 3) / 4) * ntj, cu, 2.0},
+                {3, ns * ((np + 1) / 2) * ntj, cu, 1.0},
+                {1, ns * np * 2 * ntj, 3 * cu, 0.8},
+                {2, ns * np * 4 * ntj, 4 * cu, 0.6}};
+  TileChoice tc{0, false};
+  double best = 1e300;
+  for (const Cand& c : cands) {
+    const double est = (double)((c.wgs + c.slots - 1) / c.slots) * c.t;
+    if (est < best - 1e-9) {
+      best = est;
+      tc.wta = c.id;
+    }
+  }
+  tc.ahtw_small = np * e->ngt < cu;
+  if (e->force_wta >= 0) tc.wta = e->force_wta;   // NMFC_WTA_TILE (tests: every shape gives the same bits)
+  if (e->force_ahtw >= 0) tc.ahtw_small = e->force_ahtw == 1;
+  return tc;
+}
 
 hipEvent_t take_event(nmfc_engine* e) {
   if (!e->ev_pool.empty()) {
@@ -620,18 +669,9 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     if (it < opts.maxiter) {
       const int chunk = std::min(opts.check_every, opts.maxiter - it);
       // tile shapes by grid size (a speed choice only: every shape sums in the canonical K order)
-      bool wta_big = (long)e->nsplit * (pk.npanels / WTA_NPT) * ntj >= 2L * e->ncu;
-      // 2-panel x 128-sample tiles (8 waves) while they still give every CU a workgroup
-      bool wta_mid = !wta_big && (long)e->nsplit * (pk.npanels / 2) * ntj >= (long)e->ncu;
-      bool wta_tiny = !wta_big && !wta_mid && (long)e->nsplit * pk.npanels * 2 * ntj <= 2L * e->ncu;
-      // A h^T tiles: 1 panel x 128 genes, or 1 panel x 64 genes for small grids (twice the workgroups)
-      bool ahtw_small = (long)pk.npanels * e->ngt <= 8L * e->ncu;
-      if (e->force_wta >= 0) {   // NMFC_WTA_TILE (tests: every shape must give the same bits)
-        wta_big = e->force_wta == 0;
-        wta_tiny = e->force_wta == 2;
-        wta_mid = e->force_wta == 3;
-      }
-      if (e->force_ahtw >= 0) ahtw_small = e->force_ahtw == 1;
+      const TileChoice tc = choose_tiles(e, live_panels(pk), ntj);
+      bool wta_big = tc.wta == 0, wta_mid = tc.wta == 3, wta_tiny = tc.wta == 2;
+      bool ahtw_small = tc.ahtw_small;
       const int ngt_ahtw = e->ngt * (ahtw_small ? 2 : 1);
       const int grid_ahtw = pk.npanels * ngt_ahtw;
       for (int c = 1; c <= chunk; ++c) {

@@ -682,33 +682,40 @@ __device__ __forceinline__ void ahtw_map(int item, int npanels, int ngt, int& p,
 }
 
 // ---------------------------------------------------------------------------------------------
-// K3 v4 "ahtw4": F = A h^T on the 3-stage GTile ring (one panel x 128 genes, 4 waves 1 x 4, 72 KiB)
-// + 8 KiB of h h^T rows = 80 KiB: two workgroups per CU.  Column state lives in registers: each wave
-// reads the panel's 64 ColInfo entries (lane = column), the active set is a 64-bit ballot of
-// colact[c] == iter (k_hupdate stamps its restart's columns with the iteration it ran) and the
-// E-operand rows' (lc0, k) come by lane shuffles.  These setup loads are issued after the first DMA
-// stages, so they overlap them.  The h h^T rows are read from SHP (panel-row layout
-// written by k_hupdate), one coalesced 8 KiB block.  W0 is loaded in the D layout right after the
-// last DMA issue (two stages before the end) and is the B operand of E = W0 (h h^T) directly.
+// K3 v4 "ahtw4": F = A h^T on the GTile ring (NPT panels x GTG genes, 4 waves per panel: WR = NPT,
+// WC = 4, each wave 64 panel rows x GTG/4 genes) + the panels' h h^T rows in LDS.  NPT = 1, GTG = 128,
+// 3 stages: 72 + 8 KiB, two workgroups per CU; NPT = 2 halves the A-tile bytes per flop (one A tile feeds
+// two panels) at one workgroup of 8 waves per CU.  Column state lives in registers: each wave reads its
+// panel's 64 ColInfo entries (lane = column), the active set is a 64-bit ballot of colact[c] == iter
+// (k_hupdate stamps its restart's columns with the iteration it ran) and the E-operand rows' (lc0, k)
+// come by lane shuffles.  These setup loads are issued after the first DMA stages, so they overlap
+// them.  The h h^T rows are read from SHP (panel-row layout written by k_hupdate), one coalesced
+// block.  W0 is loaded in the D layout right after the last DMA issue and is the B operand of
+// E = W0 (h h^T) directly.
 // ---------------------------------------------------------------------------------------------
 // GTG: genes per tile (128 at full load; 64 for small grids: half the MFMA chain per wave, twice the
-// workgroups).  ngt = m_pad / GTG.  Every shape accumulates in the canonical GTile K order.
-template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF>
-static __global__ __launch_bounds__(256, (GTile<64, GTG, 1, 4, NBUF>::LDS_BYTES + PANEL * KMAX * 8 <= 81920) ? 2 : 1)
-void k_ahtw4(int iter, const double* __restrict__ H, long n_pad,
-                                                         const double* __restrict__ Arm, long m_pad,
-                                                         double* __restrict__ W, const double* __restrict__ SHP,
-                                                         const ColInfo* __restrict__ ci,
-                                                         const int* __restrict__ colact, int npanels, int ngt) {
-  using TileW4 = GTile<64, GTG, 1, 4, NBUF>;
+// workgroups).  ngt = m_pad / GTG; npanels is a multiple of NPT.  Every shape accumulates in the
+// canonical GTile K order.
+template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1>
+static __global__ __launch_bounds__(256 * NPT,
+                                    (GTile<64 * NPT, GTG, NPT, 4, NBUF>::LDS_BYTES + NPT * PANEL * KMAX * 8 <= 81920)
+                                        ? 2 * NPT
+                                        : NPT)
+void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* __restrict__ Arm, long m_pad,
+             double* __restrict__ W, const double* __restrict__ SHP, const ColInfo* __restrict__ ci,
+             const int* __restrict__ colact, int npanels, int ngt) {
+  using TileW4 = GTile<64 * NPT, GTG, NPT, 4, NBUF>;
   constexpr int AHTW4_SH = TileW4::LDS_BYTES;
-  constexpr int AHTW4_LDS = AHTW4_SH + PANEL * KMAX * 8;
+  constexpr int AHTW4_LDS = AHTW4_SH + NPT * PANEL * KMAX * 8;
   static_assert(AHTW4_LDS <= 163840, "LDS of one CU");
+  constexpr int NTH = 256 * NPT;
   __shared__ __attribute__((aligned(1024))) char smem[AHTW4_LDS];
   double* SHl = reinterpret_cast<double*>(smem + AHTW4_SH);
-  int p, gt;
-  ahtw_map(xcd_item(blockIdx.x, npanels * ngt), npanels, ngt, p, gt);
-  const int tid = threadIdx.x, lane = tid & 63, wc = tid >> 6;
+  int pp, gt;
+  ahtw_map(xcd_item(blockIdx.x, (npanels / NPT) * ngt), npanels / NPT, ngt, pp, gt);
+  const int p0 = pp * NPT;   // first panel of the tile
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3;
+  const int p = p0 + wr;     // this wave's panel
   ColInfo cc;
   uint64_t actmask = 0;
   TileW4 tl;
@@ -716,19 +723,27 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad,
   const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / 4) * wc + (lane & 15);
   double w0[TileW4::MB][TileW4::NB][4];
   const bool live = tl.template run<TileW4::MB * TileW4::NB * 4>(
-      H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
+      H + (long)p0 * PANEL * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
       [&] {   // setup loads, independent of each other, overlapping the first stages' DMA
         cc = ci[(long)p * PANEL + lane];
-        const int ca = colact[(long)p * PANEL + lane];
-        const d2* src = reinterpret_cast<const d2*>(SHP + (long)p * PANEL * KMAX);
-        constexpr int NSH = PANEL * KMAX / 2 / 256;
+        int ca[NPT];
+#pragma unroll
+        for (int q = 0; q < NPT; ++q) ca[q] = colact[(long)(p0 + q) * PANEL + lane];
+        const d2* src = reinterpret_cast<const d2*>(SHP + (long)p0 * PANEL * KMAX);
+        constexpr int NSH = NPT * PANEL * KMAX / 2 / NTH;
         d2 shv[NSH];
 #pragma unroll
-        for (int j = 0; j < NSH; ++j) shv[j] = src[tid + 256 * j];
-        actmask = __ballot(ca == iter);   // the column's restart ran k_hupdate at this iteration
-        if (actmask == 0) return false;   // idle panel (the same answer in every wave)
+        for (int j = 0; j < NSH; ++j) shv[j] = src[tid + NTH * j];
+        bool any = false;
 #pragma unroll
-        for (int j = 0; j < NSH; ++j) reinterpret_cast<d2*>(SHl)[tid + 256 * j] = shv[j];
+        for (int q = 0; q < NPT; ++q) {
+          const uint64_t mk = __ballot(ca[q] == iter);   // the column's restart ran k_hupdate at this iteration
+          if (q == wr) actmask = mk;
+          any = any || mk != 0;
+        }
+        if (!any) return false;   // every panel of the tile idle (the same answer in every wave)
+#pragma unroll
+        for (int j = 0; j < NSH; ++j) reinterpret_cast<d2*>(SHl)[tid + NTH * j] = shv[j];
         return true;   // SHl is published by the ring prologue's barrier
       },
       [](const char*) {},
@@ -744,7 +759,9 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad,
                                     : wsrc[(long)(16 * mb + (lane >> 4) + 4 * reg) * m_pad + 16 * nb];
       });
   if (!live) return;
+  if (actmask == 0) return;   // this wave's panel is idle (its partner panel is not)
   double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / 4) * wc + (lane & 15);
+  const double* SHw = SHl + (long)wr * PANEL * KMAX;
 #pragma unroll
   for (int mb = 0; mb < TileW4::MB; ++mb) {
     const int ra = 16 * mb + (lane & 15);
@@ -765,7 +782,7 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad,
     for (int q = 0; q < 16; ++q) {
       if (4 * q + 3 < lo || 4 * q >= hi) continue;   // wave-uniform
       const int bb = 4 * q + (lane >> 4) - alc;
-      const double av = (bb >= 0 && bb < ak) ? SHl[ra * KMAX + bb] : 0.0;
+      const double av = (bb >= 0 && bb < ak) ? SHw[ra * KMAX + bb] : 0.0;
 #pragma unroll
       for (int nb = 0; nb < TileW4::NB; ++nb)
         e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, w0[q >> 2][nb][q & 3], e[nb], 0, 0, 0);

@@ -113,6 +113,15 @@ int main() {
     CK(hipEventElapsedTime(&ms, e0, e1));
     fl = 256.0 * iters * 4 * 2048.0;
     printf("mfma f64 one wave/CU 4 acc: %.3f ms -> %.1f cycles/mfma @2.4GHz\n", ms, ms * 1e-3 * 2.4e9 / (iters * 4.0));
+    for (int na = 1; na <= 4; na *= 2) {   // one wave per SIMD: cycles per MFMA with na independent chains
+      CK(hipEventRecord(e0));
+      if (na == 1) rate_k<1><<<256, 256>>>(dout, iters, 1.0);
+      if (na == 2) rate_k<2><<<256, 256>>>(dout, iters, 1.0);
+      if (na == 4) rate_k<4><<<256, 256>>>(dout, iters, 1.0);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("mfma f64 one wave/SIMD, %d chain(s): %.1f cycles/mfma @2.4GHz\n", na, ms * 1e-3 * 2.4e9 / (iters * (double)na));
+    }
     CK(hipEventRecord(e0)); valu_k<<<blocks, threads>>>(dout, iters, 1.0); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1));
     fl = (double)blocks * threads * iters * 8 * 2.0;

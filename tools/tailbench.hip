@@ -207,6 +207,32 @@ int main(int argc, char** argv) {
     report("ahtw4 128 nbuf4", timeit([&] {
              hipLaunchKernelGGL((k_ahtw4<0, 128, 4>), dim3(npanels * ngt), dim3(256), 0, 0, AHTW_ARGS(ngt));
            }, reps));
+    report("ahtw4 2x128 nbuf3 (8w)", timeit([&] {
+             hipLaunchKernelGGL((k_ahtw4<0, 128, 3, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
+           }, reps));
+    report("ahtw4 2x128 nbuf4 (8w)", timeit([&] {
+             hipLaunchKernelGGL((k_ahtw4<0, 128, 4, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
+           }, reps));
+    report("ahtw4 2x64 nbuf3 (8w)", timeit([&] {
+             hipLaunchKernelGGL((k_ahtw4<0, 64, 3, 2>), dim3(npanels / 2 * 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(2 * ngt));
+           }, reps));
+    {   // bit-identity of the 2-panel tile against the 1-panel tile (same canonical K order)
+      const size_t nw = (size_t)npanels * PANEL * m_pad;
+      std::vector<double> w1(nw), w2(nw), w0(nw);
+      CK(hipMemcpy(w0.data(), W, nw * 8, hipMemcpyDeviceToHost));
+      hipLaunchKernelGGL((k_ahtw4<0, 128, 3>), dim3(npanels * ngt), dim3(256), 0, 0, AHTW_ARGS(ngt));
+      CK(hipMemcpy(w1.data(), W, nw * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(W, w0.data(), nw * 8, hipMemcpyHostToDevice));
+      hipLaunchKernelGGL((k_ahtw4<0, 128, 3, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
+      CK(hipMemcpy(w2.data(), W, nw * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(W, w0.data(), nw * 8, hipMemcpyHostToDevice));
+      size_t diff = 0, changed = 0;
+      for (size_t i = 0; i < nw; ++i) {
+        diff += (w1[i] != w2[i]);
+        changed += (w1[i] != w0[i]);
+      }
+      printf("  ahtw4 2-panel vs 1-panel: %zu of %zu W entries differ (%zu updated)\n", diff, nw, changed);
+    }
   }
   printf("\ndone\n");
   return 0;
