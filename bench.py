@@ -144,6 +144,7 @@ def main():
                     help="strong (default): the fixed R restarts per k are split over the N GPUs (the north-star "
                          "job); weak: every GPU runs the full per-GPU workload (R restarts per k each, consensus "
                          "over R x N).  C4 is always weak (the per-GPU share of configs[3])")
+    ap.add_argument("--dump-iters", default=None, help="write the last step's per-job iteration counts (.npy)")
     ap.add_argument("--cpu-kind", default="reference", choices=["reference", "port"],
                     help="reference: the reference's own nmf_mu (oracle/_ref, fails loudly when absent); port: the "
                          "oracle's C restatement")
@@ -238,6 +239,8 @@ def main():
         elapsed = float(t.item())
 
     res, rho = last
+    if args.dump_iters and rank == 0:
+        np.save(args.dump_iters, np.stack([np.asarray(ks)[np.arange(jb, je) % nk], res.iters]))
     total_restarts = nk * R * args.steps
     value = total_restarts / elapsed
     its = np.concatenate(iters_all)

@@ -154,8 +154,10 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
 int nmfc_calculate_norm_dev(const double* da, const double* dw, const double* dh, double* dd, int m, int n, int k,
                             double* norm_out, double* ms_out) {
   if (!da || !dw || !dh || !dd || m <= 0 || n <= 0 || k <= 0 || !norm_out) return -1;
-  const size_t la = (size_t)m * n;
-  const int blocks = (int)std::min<size_t>((la + nmfc::NT - 1) / nmfc::NT, NORM_BLOCKS);
+  // grid: gene blocks x column groups (>> 256 CUs of workgroups; fixed for (m, n): deterministic sum order)
+  const int gx = (m + nmfc::NT - 1) / nmfc::NT;
+  const int gy = std::max(1, std::min(n, (int)((NORM_BLOCKS + gx - 1) / gx)));
+  const int blocks = gx * gy;
   std::vector<double> part(blocks);
   double* dp = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
@@ -163,7 +165,7 @@ int nmfc_calculate_norm_dev(const double* da, const double* dw, const double* dh
   if (hipMalloc(&dp, blocks * 8) != hipSuccess) goto done;
   if (ms_out && (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess)) goto done;
   if (ms_out) (void)hipEventRecord(ev[0], 0);
-  hipLaunchKernelGGL(nmfc::k_norm_partial, dim3(blocks), dim3(nmfc::NT), 0, 0, da, dw, dh, dd, m, n, k, dp);
+  hipLaunchKernelGGL(nmfc::k_norm_partial, dim3(gx, gy), dim3(nmfc::NT), 0, 0, da, dw, dh, dd, m, n, k, dp);
   if (hipGetLastError() != hipSuccess) goto done;
   if (ms_out) (void)hipEventRecord(ev[1], 0);
   if (hipMemcpy(part.data(), dp, blocks * 8, hipMemcpyDeviceToHost) != hipSuccess) goto done;

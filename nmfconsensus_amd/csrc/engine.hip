@@ -714,7 +714,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         }
         {
           TimedLaunch tl(e, KID_HUPD);
-          hipLaunchKernelGGL(k_hupdate, dim3(nact), dim3(NT), 0, st, iter, opts.maxiter, opts.stop_rule,
+          hipLaunchKernelGGL(k_hupdate, dim3(nact), dim3(NTH), 0, st, iter, opts.maxiter, opts.stop_rule,
                              e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, e->nsplit,
                              e->SWpart.as<double>(), sw_total, e->H[cur].as<double>(), e->SH.as<double>(),
                              e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->unchanged.as<int>(),
@@ -844,7 +844,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     }
     {
       TimedLaunch tl(e, KID_COUNTS);
-      hipLaunchKernelGGL(k_counts, dim3((n + 15) / 16, (n + 15) / 16, nk), dim3(NT), 0, st, e->labels.as<int32_t>(),
+      hipLaunchKernelGGL(k_counts, dim3((n + CNT_T - 1) / CNT_T, (n + CNT_T - 1) / CNT_T, nk), dim3(NT), 0, st, e->labels.as<int32_t>(),
                          e->grp_begin.as<int>(), e->grp_list.as<int>(), n, dcounts);
     }
     HCHECK(hipGetLastError());
@@ -982,7 +982,7 @@ int nmfc_consensus(const double* Hs, int k, int n, int R, int label_rule, int32_
   hipLaunchKernelGGL(k_labels, dim3((n + NT - 1) / NT, R), dim3(NT), 0, 0, dri.as<RestartInfo>(), dslot.as<int>(),
                      dH.as<double>(), (long)n, n, label_rule, dlab.as<int32_t>());
   HCHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_counts, dim3((n + 15) / 16, (n + 15) / 16, 1), dim3(NT), 0, 0, dlab.as<int32_t>(), dgb.as<int>(),
+  hipLaunchKernelGGL(k_counts, dim3((n + CNT_T - 1) / CNT_T, (n + CNT_T - 1) / CNT_T, 1), dim3(NT), 0, 0, dlab.as<int32_t>(), dgb.as<int>(),
                      dslot.as<int>(), n, dcnt.as<int32_t>());
   HCHECK(hipGetLastError());
   hipLaunchKernelGGL(k_divide, dim3((unsigned)(((size_t)n * n + NT - 1) / NT)), dim3(NT), 0, 0, dcnt.as<int32_t>(),

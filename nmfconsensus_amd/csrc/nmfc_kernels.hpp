@@ -24,7 +24,6 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 constexpr int PANEL = 64;          // restart columns per panel
 constexpr int BK = 32;             // padding multiple of the sample dimension (K of A h^T)
 constexpr int NT = 256;            // threads per workgroup
-constexpr int HCH = 256;           // sample chunk of the H-update kernel
 constexpr int KMAX = 16;           // largest rank k
 constexpr int GT = 128;            // genes per A h^T tile (and per Gram partial)
 constexpr int STOP_FIXED = 0, STOP_REF_COMPAT = 1, STOP_ARGMAX_STABLE = 2, STOP_TOLX = 3;
@@ -432,17 +431,24 @@ static __global__ __launch_bounds__(WR * WC * 64) void k_wta2(const double* __re
 //   work1 = W0^T W0 = sum of the per-chunk Gram partials (nmf_mu.c:176); work2 = work1 H0 (:178);
 //   H <- mu_rule(H, G, work2) (:184-191); SH = H H^T (:200); stability check (:253-282).
 // ---------------------------------------------------------------------------------------------
+constexpr int NTH = 512;           // threads of the H-update kernel (one sample per thread and round)
+constexpr int HCH2 = NTH;          // samples per round
+
 struct HupdSmem {
   double sw[KMAX * KMAX];
-  double Hn[KMAX * HCH];
+  double Hn[KMAX * HCH2];
   double win[KMAX * KMAX];
-  double shp[NT];
+  double shp[NTH];
   int changed;
   unsigned long long dmax, omax;   // STOP_TOLX: max |h0 - h| and max |h0| (non-negative doubles as bits)
 };
 
-// The body for rank K (compile time): every per-sample loop over the k factors is unrolled, so the
-// k loads of one chunk round are issued together and consumed after.
+// The body for rank K (compile time).  Latency is what matters here (one workgroup per restart, often
+// only a few restarts live): every load the workgroup needs is issued before its first use -- the stop
+// state, the Gram partials and the first round's H and W^T A partials together -- and the split-K
+// partials of one sample are loaded GS chunks at a time (GS*K <= 64 values in flight per thread).  The
+// arithmetic order is fixed: chunk partials and Gram partials summed in chunk order, d = sum_b in b order,
+// h h^T by T = f(k) threads per pair over j = pq (mod T) in j order, then the T partials in pq order.
 template <int K>
 __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int maxiter, int stop_rule, int n,
                                              long n_pad, const double* __restrict__ Gpart, long g_ld, long g_split,
@@ -452,6 +458,7 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
                                              int* __restrict__ unchanged, int* __restrict__ classes, long cls_ld,
                                              int* __restrict__ n_stopped, double* __restrict__ SHP,
                                              int* __restrict__ colact, double* __restrict__ Hstat, HupdSmem& sm) {
+  constexpr int GS = (64 / K) < 1 ? 1 : (64 / K) > 16 ? 16 : (64 / K);
   double* sw = sm.sw;
   double* Hn = sm.Hn;
   double* win = sm.win;
@@ -464,29 +471,57 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
   const bool check = (stop_rule != STOP_FIXED) && iter > 1 && (iter % 2 == 0);
   const bool tolx = check && stop_rule == STOP_TOLX;
   double tdm = 0.0, tom = 0.0;   // this thread's max |h0 - h| and max |h0| (STOP_TOLX)
+  // stop state, loaded now and used at the end
+  const int u_prev = (tid == 0 && check) ? unchanged[rid] : 0;
+  const int nwin = k < n ? k : n;
+  const bool refc = check && stop_rule == STOP_REF_COMPAT;
+  const int cl_prev = (refc && tid < nwin) ? classes[(long)rid * cls_ld + tid] : 0;
+  // the sample rounds' loads: H and the split-K partials of W^T A (first group issued here)
+  auto load_h = [&](int j, double* hc) {
+#pragma unroll
+    for (int a = 0; a < K; ++a) hc[a] = H[(long)(c0 + a) * n_pad + j];
+  };
+  auto sum_g = [&](int j, double* gs) {   // chunk partials of this sample, added in chunk order
+    const double* gsrc = Gpart + (long)c0 * g_ld + j;
+    for (int g0 = 0; g0 < nsplit; g0 += GS) {
+      double v[GS][K];
+#pragma unroll
+      for (int u = 0; u < GS; ++u) {   // chunks past the end re-read the last one (not added)
+        const double* q = gsrc + (long)min(g0 + u, nsplit - 1) * g_split;
+#pragma unroll
+        for (int a = 0; a < K; ++a) v[u][a] = q[(long)a * g_ld];
+      }
+#pragma unroll
+      for (int u = 0; u < GS; ++u)
+        if (g0 + u < nsplit) {
+#pragma unroll
+          for (int a = 0; a < K; ++a) gs[a] = (g0 + u == 0) ? v[u][a] : gs[a] + v[u][a];
+        }
+    }
+  };
   if (tid == 0) {
     changed = 0;
     sm.dmax = 0ull;
     sm.omax = 0ull;
   }
-  for (int idx = tid; idx < k * k; idx += NT) {
+  for (int idx = tid; idx < k * k; idx += NTH) {
     const double* src = SWpart + me.sq_off + idx;
     double sacc = 0.0;
-    for (int g0 = 0; g0 < nsplit; g0 += 8) {
-      double v[8];
+    for (int g0 = 0; g0 < nsplit; g0 += 16) {
+      double v[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = (g0 + u < nsplit) ? src[(long)(g0 + u) * sw_total] : 0.0;
+      for (int u = 0; u < 16; ++u) v[u] = (g0 + u < nsplit) ? src[(long)(g0 + u) * sw_total] : 0.0;
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < 16; ++u)
         if (g0 + u < nsplit) sacc = (g0 + u == 0) ? v[u] : sacc + v[u];
     }
     sw[(idx / k) * KMAX + (idx % k)] = sacc;
   }
-  for (int idx = tid; idx < KMAX * KMAX; idx += NT) win[idx] = 0.0;
+  for (int idx = tid; idx < KMAX * KMAX; idx += NTH) win[idx] = 0.0;
   // h h^T: T threads per (pa, pb) pair (T a function of k only); thread pq of a pair sums the samples
   // j = pq (mod T) in order, and the T partials are added in pq order at the end.
   const int npairs = k * (k + 1) / 2;
-  const int T = (npairs * 8 <= NT) ? 8 : (npairs * 4 <= NT) ? 4 : (npairs * 2 <= NT) ? 2 : 1;
+  const int T = (npairs * 8 <= 256) ? 8 : (npairs * 4 <= 256) ? 4 : (npairs * 2 <= 256) ? 2 : 1;
   const int pid = tid / T, pq = tid % T;
   int pa = 0, pb = 0;
   if (pid < npairs) {
@@ -498,40 +533,23 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
     pb = pa + t;
   }
   double shacc = 0.0;
-  __syncthreads();
 
-  for (int j0 = 0; j0 < n; j0 += HCH) {
+  for (int j0 = 0; j0 < n; j0 += HCH2) {
     const int j = j0 + tid;
     const bool valid = j < n;
-    // this sample's k entries of H and of the chunk-summed W^T A (partials added in chunk order);
-    // the k loads of one chunk round are independent, so they are in flight together
     double hc[K], gs[K];
 #pragma unroll
     for (int a = 0; a < K; ++a) {
-      hc[a] = valid ? H[(long)(c0 + a) * n_pad + j] : 0.0;
+      hc[a] = 0.0;
       gs[a] = 0.0;
     }
+    int cl_j = 0;
     if (valid) {
-      const double* gsrc = Gpart + (long)c0 * g_ld + j;
-      int sp = 0;
-      for (; sp + 1 < nsplit; sp += 2) {   // two chunk rounds: 2K independent loads, then the adds
-        double v0[K], v1[K];
-#pragma unroll
-        for (int a = 0; a < K; ++a) {
-          v0[a] = gsrc[(long)sp * g_split + (long)a * g_ld];
-          v1[a] = gsrc[(long)(sp + 1) * g_split + (long)a * g_ld];
-        }
-#pragma unroll
-        for (int a = 0; a < K; ++a) gs[a] = ((sp == 0) ? v0[a] : gs[a] + v0[a]) + v1[a];
-      }
-      if (sp < nsplit) {
-        double v0[K];
-#pragma unroll
-        for (int a = 0; a < K; ++a) v0[a] = gsrc[(long)sp * g_split + (long)a * g_ld];
-#pragma unroll
-        for (int a = 0; a < K; ++a) gs[a] = (sp == 0) ? v0[a] : gs[a] + v0[a];
-      }
+      load_h(j, hc);
+      if (check && stop_rule == STOP_ARGMAX_STABLE) cl_j = classes[(long)rid * cls_ld + j];
+      sum_g(j, gs);
     }
+    __syncthreads();   // sw, win (first round) / Hn free (later rounds)
     int best = 0;
     double bestv = 0.0;
 #pragma unroll
@@ -547,37 +565,31 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
           tdm = fmax(tdm, fabs(hc[a] - hn));
           tom = fmax(tom, fabs(hc[a]));
         }
-        if (stop_rule == STOP_REF_COMPAT) {
+        if (refc) {
           // flat column-major index of (a, j) in the k x n buffer; window i reads [i*n, i*n + k)
-          const long tf = (long)j * k + a;
-          const long wi = tf / n;
-          if (wi < k) {
-            const long wj = tf - wi * n;
-            if (wj < k) win[wi * KMAX + wj] = hn;
-          }
+          const int tf = j * k + a;
+          const int wi = tf / n;
+          const int wj = tf - wi * n;
+          if (wi < k && wj < k) win[wi * KMAX + wj] = hn;
         }
       }
-      Hn[a * HCH + tid] = hn;
+      Hn[a * HCH2 + tid] = hn;
       if (a == 0 || hn > bestv) {   // first maximum
         best = a;
         bestv = hn;
       }
     }
-    if (check && stop_rule == STOP_ARGMAX_STABLE && valid) {
-      int* cl = classes + (long)rid * cls_ld + j;
-      if (*cl != best) {
-        *cl = best;
-        changed = 1;
-      }
+    if (check && stop_rule == STOP_ARGMAX_STABLE && valid && cl_j != best) {
+      classes[(long)rid * cls_ld + j] = best;
+      changed = 1;
     }
     __syncthreads();
     if (pid < npairs) {
-      const int cnt = min(HCH, n - j0);
-      const double* ha = Hn + pa * HCH;
-      const double* hb = Hn + pb * HCH;
+      const int cnt = min(HCH2, n - j0);
+      const double* ha = Hn + pa * HCH2;
+      const double* hb = Hn + pb * HCH2;
       for (int q = pq; q < cnt; q += T) shacc = fma(ha[q], hb[q], shacc);
     }
-    __syncthreads();
   }
   shp[tid] = shacc;
   if (tolx) {
@@ -598,17 +610,13 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
     }
   }
   if (colact && tid < k) colact[c0 + tid] = iter;   // this restart's columns take part in the W update
-  if (check && stop_rule == STOP_REF_COMPAT) {
-    const int nwin = k < n ? k : n;
-    if (tid < nwin) {
-      int c = 0;
-      for (int jj = 1; jj < k; ++jj)
-        if (win[tid * KMAX + jj] > win[tid * KMAX + jj - 1]) c = jj;
-      int* cl = classes + (long)rid * cls_ld + tid;
-      if (*cl != c) {
-        *cl = c;
-        changed = 1;
-      }
+  if (refc && tid < nwin) {
+    int c = 0;
+    for (int jj = 1; jj < k; ++jj)
+      if (win[tid * KMAX + jj] > win[tid * KMAX + jj - 1]) c = jj;
+    if (cl_prev != c) {
+      classes[(long)rid * cls_ld + tid] = c;
+      changed = 1;
     }
   }
   __syncthreads();
@@ -616,7 +624,7 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
     int reason = 0;
     if (check && stop_rule != STOP_TOLX) {   // the TolX test runs after the W update (k_wstat)
       if (!changed) {
-        const int u = unchanged[rid] + 1;
+        const int u = u_prev + 1;
         unchanged[rid] = u;
         if (u >= 200) reason = 1;   // nmf_mu.c:269-271
       } else {
@@ -632,16 +640,16 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
   }
 }
 
-static __global__ __launch_bounds__(NT) void k_hupdate(int iter, int maxiter, int stop_rule,
-                                                       const RestartInfo* __restrict__ ri, int n, long n_pad,
-                                                       const double* __restrict__ Gpart, long g_ld, long g_split,
-                                                       int nsplit, const double* __restrict__ SWpart, long sw_total,
-                                                       double* __restrict__ H, double* __restrict__ SH,
-                                                       int* __restrict__ stop_iter, int* __restrict__ stop_reason,
-                                                       int* __restrict__ unchanged, int* __restrict__ classes,
-                                                       long cls_ld, int* __restrict__ n_stopped,
-                                                       double* __restrict__ SHP, int* __restrict__ colact,
-                                                       double* __restrict__ Hstat) {
+static __global__ __launch_bounds__(NTH) void k_hupdate(int iter, int maxiter, int stop_rule,
+                                                        const RestartInfo* __restrict__ ri, int n, long n_pad,
+                                                        const double* __restrict__ Gpart, long g_ld, long g_split,
+                                                        int nsplit, const double* __restrict__ SWpart, long sw_total,
+                                                        double* __restrict__ H, double* __restrict__ SH,
+                                                        int* __restrict__ stop_iter, int* __restrict__ stop_reason,
+                                                        int* __restrict__ unchanged, int* __restrict__ classes,
+                                                        long cls_ld, int* __restrict__ n_stopped,
+                                                        double* __restrict__ SHP, int* __restrict__ colact,
+                                                        double* __restrict__ Hstat) {
   __shared__ HupdSmem sm;
   const RestartInfo me = ri[blockIdx.x];
   if (stop_iter[me.rid] != 0) return;
@@ -1009,22 +1017,53 @@ static __global__ __launch_bounds__(NT) void k_labels(const RestartInfo* __restr
   labels[(long)slot[r] * n + j] = best + 1;
 }
 
-// counts[g][i + j*n] = sum over the group's restarts of [L[i] == L[j]]
+// counts[g][i + j*n] = sum over the group's restarts of [L[i] == L[j]] (nmf.r:140-141).  A workgroup owns a
+// 64 x 64 block of (i, j); the two 64-label strips of CR restarts at a time are staged in LDS (each label
+// read once per block) and every thread accumulates a 4 x 4 register block of exact integer counts.
+constexpr int CNT_T = 64, CNT_R = 32;
 static __global__ __launch_bounds__(NT) void k_counts(const int32_t* __restrict__ labels,
                                                       const int* __restrict__ grp_begin,
                                                       const int* __restrict__ grp_list, int n,
                                                       int32_t* __restrict__ counts) {
+  __shared__ int32_t li[CNT_R][CNT_T], lj[CNT_R][CNT_T];
   const int gidx = blockIdx.z;
-  const int i = blockIdx.x * 16 + (threadIdx.x & 15);
-  const int j = blockIdx.y * 16 + (threadIdx.x >> 4);
-  if (i >= n || j >= n) return;
+  const int i0 = blockIdx.x * CNT_T, j0 = blockIdx.y * CNT_T;
+  const int tid = threadIdx.x, ti = (tid & 15) * 4, tj = (tid >> 4) * 4;
   const int b = grp_begin[gidx], e = grp_begin[gidx + 1];
-  int32_t cnt = 0;
-  for (int q = b; q < e; ++q) {
-    const int32_t* L = labels + (long)grp_list[q] * n;
-    cnt += (L[i] == L[j]);
+  int32_t cnt[4][4] = {};
+  for (int q0 = b; q0 < e; q0 += CNT_R) {
+    const int nr = min(CNT_R, e - q0);
+    for (int x = tid; x < nr * CNT_T; x += NT) {
+      const int r = x / CNT_T, c = x % CNT_T;
+      const int32_t* L = labels + (long)grp_list[q0 + r] * n;
+      li[r][c] = (i0 + c < n) ? L[i0 + c] : -1;
+      lj[r][c] = (j0 + c < n) ? L[j0 + c] : -2;
+    }
+    __syncthreads();
+    for (int r = 0; r < nr; ++r) {
+      int32_t a[4], bb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = li[r][ti + u];
+        bb[u] = lj[r][tj + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) cnt[u][v] += (a[u] == bb[v]);
+    }
+    __syncthreads();
   }
-  counts[(long)gidx * n * n + (long)j * n + i] = cnt;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int j = j0 + tj + v;
+    if (j >= n) continue;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + ti + u;
+      if (i < n) counts[(long)gidx * n * n + (long)j * n + i] = cnt[u][v];
+    }
+  }
 }
 
 static __global__ void k_divide(const int32_t* __restrict__ counts, double denom, long len, double* __restrict__ out) {
@@ -1046,19 +1085,22 @@ static __global__ void k_layout_a(const double* __restrict__ A, long lda, int m,
 // ---------------------------------------------------------------------------------------------
 // calculateNorm (calculatenorm.c:44-78) and calculateMaxchange (calculatemaxchange.c:42-71)
 // ---------------------------------------------------------------------------------------------
+// grid (x: gene blocks of NT, y: column groups); block (x, y) covers genes x*NT.. of columns y, y + gridDim.y, ...
 static __global__ __launch_bounds__(NT) void k_norm_partial(const double* __restrict__ a, const double* __restrict__ w,
                                                             const double* __restrict__ h, double* __restrict__ d, int m,
                                                             int n, int k, double* __restrict__ partial) {
   __shared__ double red[NT];
-  const long len = (long)m * n;
+  const int i = blockIdx.x * NT + threadIdx.x;
   double ss = 0.0;
-  for (long idx = (long)blockIdx.x * NT + threadIdx.x; idx < len; idx += (long)gridDim.x * NT) {
-    const long j = idx / m, i = idx - j * m;
-    double s = 0.0;
-    for (int q = 0; q < k; ++q) s = fma(w[i + (long)q * m], h[q + j * k], s);
-    const double v = a[idx] - s;
-    d[idx] = v;
-    ss = fma(v, v, ss);
+  if (i < m) {
+    for (int j = blockIdx.y; j < n; j += gridDim.y) {
+      const long idx = (long)j * m + i;
+      double s = 0.0;
+      for (int q = 0; q < k; ++q) s = fma(w[i + (long)q * m], h[q + (long)j * k], s);
+      const double v = a[idx] - s;
+      d[idx] = v;
+      ss = fma(v, v, ss);
+    }
   }
   red[threadIdx.x] = ss;
   __syncthreads();
@@ -1066,7 +1108,7 @@ static __global__ __launch_bounds__(NT) void k_norm_partial(const double* __rest
     if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
     __syncthreads();
   }
-  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+  if (threadIdx.x == 0) partial[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
 }
 
 static __global__ __launch_bounds__(NT) void k_maxchange_partial(const double* __restrict__ mat,

@@ -2,7 +2,9 @@
 
 Groups the MU kernels into iterations (one k_hupdate per iteration), prints per-bucket device time of
 each kernel, grid sizes, and the idle gaps between consecutive dispatches (launch/host overhead).
-Usage: python tools/trace_timeline.py <run_kernel_trace.csv> [bucket=50]"""
+Usage: python tools/trace_timeline.py <run_kernel_trace.csv> [bucket=50] [iters.npy [m n]]
+With the sweep's per-job (k, iterations) (bench.py --dump-iters), each bucket also reports the useful
+fp64 rate: sum over live restart-iterations of F = 4mnk + 4(m+n)k^2 / the bucket's span."""
 import collections
 import csv
 import sys
@@ -32,13 +34,25 @@ for s, e, nm, g in rows:
     sp = span[b]
     sp[0] = s if sp[0] is None else sp[0]
     sp[1] = e
+useful = None
+if len(sys.argv) > 3:
+    import numpy as np
+    kk, its = np.load(sys.argv[3])
+    mm = int(sys.argv[4]) if len(sys.argv) > 4 else 20000
+    nn = int(sys.argv[5]) if len(sys.argv) > 5 else 500
+    F = 4.0 * mm * nn * kk + 4.0 * (mm + nn) * kk * kk
+    useful = {}
+    for b in agg:
+        lo, hi = b * bucket, (b + 1) * bucket
+        useful[b] = float(np.sum(F * np.clip(its - lo, 0, hi - lo)))
 tot = 0.0
-print(f"{'iters':>11s} {'span ms':>8s} {'gap ms':>7s}  kernels (ms, mean grid)")
+print(f"{'iters':>11s} {'span ms':>8s} {'gap ms':>7s} {'TF':>6s}  kernels (ms, mean grid)")
 for b in sorted(agg):
     sp = (span[b][1] - span[b][0]) / 1e6
     tot += sp
     parts = "  ".join(f"{k}={v:.1f}({sum(grids[b][k]) / len(grids[b][k]):.0f})" for k, v in sorted(agg[b].items()) if v > 0.05)
-    print(f"{b * bucket:5d}-{(b + 1) * bucket:5d} {sp:8.1f} {gap[b]:7.2f}  {parts}")
+    tf = useful[b] / (sp * 1e-3) / 1e12 if useful else float("nan")
+    print(f"{b * bucket:5d}-{(b + 1) * bucket:5d} {sp:8.1f} {gap[b]:7.2f} {tf:6.1f}  {parts}")
 print(f"total span {tot:.1f} ms over {it} iterations")
 gaps = sorted(((rows[i + 1][0] - rows[i][1], i) for i in range(len(rows) - 1)), reverse=True)
 print("largest idle gaps:")
