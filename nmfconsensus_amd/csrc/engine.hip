@@ -172,6 +172,14 @@ Packing pack(const std::vector<RestartInfo>& in) {
   return pk;
 }
 
+// every restart of the packing lies in columns 0..15 of panel 0 (the narrow end-of-sweep kernels apply)
+bool narrow_packing(const Packing& pk) {
+  if (pk.ri.empty()) return false;
+  for (const RestartInfo& r : pk.ri)
+    if (r.col0 + r.k > 16) return false;
+  return true;
+}
+
 // panels holding at least one restart (the packing fills panels from 0; the rest pad the 4-panel groups)
 int live_panels(const Packing& pk) {
   int np = 0;
@@ -193,6 +201,8 @@ struct nmfc_engine {
   int kchunk = 0, nsplit = 0, ngt = 0;
   int ncu = 256;   // compute units (grid-size heuristics only)
   int force_wta = -1, force_ahtw = -1;   // tile-shape overrides (env NMFC_WTA_TILE / NMFC_AHTW_TILE)
+  int repack_div = 5;                     // repack after nact / repack_div stops (env NMFC_REPACK_DIV)
+  bool narrow_ok = true;                  // narrow end-of-sweep kernels allowed (env NMFC_NARROW=0 disables)
   DevBuf Acm, Arm;
   // per-run buffers (grow-only)
   DevBuf W[2], H[2], Gpart, SWpart, SH, SHP, colact, Hfin, Wfin;
@@ -355,6 +365,8 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
     const std::string v(s);
     e->force_wta = v == "big" ? 0 : v == "small" ? 1 : v == "tiny" ? 2 : v == "mid" ? 3 : -1;
   }
+  if (const char* s = getenv("NMFC_REPACK_DIV")) e->repack_div = std::max(1, atoi(s));
+  if (const char* s = getenv("NMFC_NARROW")) e->narrow_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
     const std::string v(s);
     e->force_ahtw = v == "128" ? 0 : v == "64" ? 1 : -1;
@@ -672,6 +684,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       const TileChoice tc = choose_tiles(e, live_panels(pk), ntj);
       bool wta_big = tc.wta == 0, wta_mid = tc.wta == 3, wta_tiny = tc.wta == 2;
       bool ahtw_small = tc.ahtw_small;
+      // narrow (end-of-sweep) form: every restart of the packing inside columns 0..15 of panel 0
+      const bool narrow = e->narrow_ok && narrow_packing(pk);
       const int ngt_ahtw = e->ngt * (ahtw_small ? 2 : 1);
       const int grid_ahtw = pk.npanels * ngt_ahtw;
       for (int c = 1; c <= chunk; ++c) {
@@ -681,7 +695,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           // at least twice, else 1-panel x 64-sample tiles (4 waves).  Both accumulate every entry in
           // the same canonical K order, so the switch never changes a bit.
           TimedLaunch tl(e, KID_WTA);
-          if (wta_big) {
+          if (narrow) {
+            const int ntq = (int)(e->n_cols_pad / 16);
+            hipLaunchKernelGGL((k_wta_narrow<16, 4>), dim3(e->nsplit * ntq), dim3(64), 0, st, e->W[cur].as<double>(),
+                               e->Acm.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, e->colinfo.as<ColInfo>(),
+                               e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
+          } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
             auto kw = (ntj >= 4) ? k_wta2<WTA_NPT, 128, 4, 2, 1> : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2>
                                                                             : k_wta2<WTA_NPT, 128, 4, 2, 4>;
@@ -728,11 +747,17 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                 hipMemcpyDeviceToDevice, st));
         {
           TimedLaunch tl(e, KID_AHTW);
-          auto ka = ahtw_small ? k_ahtw4<0, GT / 2> : k_ahtw4<0, GT>;
-          hipLaunchKernelGGL(ka, dim3(grid_ahtw), dim3(256), 0, st, iter,
-                             e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
-                             e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), pk.npanels,
-                             ngt_ahtw);
+          if (narrow) {   // 16 rows x 32 genes, 2 waves
+            hipLaunchKernelGGL((k_ahtw4<0, GT / 4, GT_NBUF, 1, 16, 2>), dim3(4 * e->ngt), dim3(128), 0, st, iter,
+                               e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
+                               e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), 1, 4 * e->ngt);
+          } else {
+            auto ka = ahtw_small ? k_ahtw4<0, GT / 2> : k_ahtw4<0, GT>;
+            hipLaunchKernelGGL(ka, dim3(grid_ahtw), dim3(256), 0, st, iter,
+                               e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
+                               e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), pk.npanels,
+                               ngt_ahtw);
+          }
         }
         if (tol_check) {
           TimedLaunch tl(e, KID_OTHER);
@@ -760,8 +785,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     }
     if (e->timing) drain_timing(e);
     if (done || (it >= opts.maxiter && checked == q)) break;
-    // repack when a fifth of the live restarts have stopped since the last packing
-    if (stopped - stopped_at_pack >= std::max(1, nact / 5)) {
+    // repack when a fraction 1/repack_div of the live restarts have stopped since the last packing
+    if (stopped - stopped_at_pack >= std::max(1, nact / e->repack_div)) {
       HCHECK(hipStreamSynchronize(st));
       if (e->timing) drain_timing(e);
       checked = q;   // every poll is now complete

@@ -427,6 +427,59 @@ static __global__ __launch_bounds__(WR * WC * 64) void k_wta2(const double* __re
 }
 
 // ---------------------------------------------------------------------------------------------
+// K1 narrow form (the tail: every live restart inside columns 0..15 of panel 0): G rows 0..15 = W^T A
+// over the same fixed gene chunks, one wave per (chunk, RQ-sample tile), RP = 16 rows -- a quarter of
+// the W bytes per sample tile of the 64-row tiles, so many more, lighter workgroups.  The tile's
+// accumulation is the canonical GTile K order, so the rows are bit-identical to every other shape.
+// Tile t == 0 of each chunk also forms the 16 x 16 Gram block of those columns (nmf_mu.c:176).
+// ---------------------------------------------------------------------------------------------
+template <int RQ, int NBUF>
+static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restrict__ W, const double* __restrict__ Acm,
+                                                          long m_pad, int ntq, int nsplit, int kchunk,
+                                                          const ColInfo* __restrict__ ci, double* __restrict__ Gpart,
+                                                          long g_ld, long g_split, double* __restrict__ SWpart,
+                                                          long sw_total) {
+  using T = GTile<16, RQ, 1, 1, NBUF>;
+  __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES];
+  const int item = xcd_item(blockIdx.x, nsplit * ntq);
+  const int t = item % ntq, s = item / ntq;
+  const int kbeg = s * kchunk;
+  const int kend = (int)min((long)kbeg + kchunk, m_pad);
+  const int l = threadIdx.x, fr = l & 15, g = l >> 4;
+  const bool gram = t == 0;
+  T tl;
+  tl.zero();
+  d4 gacc = (d4){0.0, 0.0, 0.0, 0.0};
+  tl.run(W, m_pad, Acm + (long)t * RQ * m_pad, m_pad, kbeg, kend, smem, [&](const char* stg) {
+    if (!gram) return;
+    const char* pa = stg + fr * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const d2 a = *reinterpret_cast<const d2*>(pa + (((4 * kk + g) ^ (fr >> 1)) << 4));
+      gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, a.x, gacc, 0, 0, 0);
+      gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, a.y, gacc, 0, 0, 0);
+    }
+  });
+  double* out = Gpart + (long)s * g_split + (long)t * RQ;
+#pragma unroll
+  for (int nb = 0; nb < T::NB; ++nb)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) out[(long)T::row_of(0, reg) * g_ld + T::col_of(nb)] = tl.acc[0][nb][reg];
+  if (gram) {
+    double* so = SWpart + (long)s * sw_total;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int lr = g + 4 * reg, lcn = fr;
+      const ColInfo cr = ci[lr];
+      if (cr.k == 0 || cr.lc0 != ci[lcn].lc0 || ci[lcn].k == 0) continue;   // not the same restart
+      const int a = lr - cr.lc0, b = lcn - cr.lc0;
+      so[cr.sq_off + a * cr.k + b] = gacc[reg];
+      so[cr.sq_off + b * cr.k + a] = gacc[reg];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // K2 "hupdate": one workgroup per active restart.
 //   work1 = W0^T W0 = sum of the per-chunk Gram partials (nmf_mu.c:176); work2 = work1 H0 (:178);
 //   H <- mu_rule(H, G, work2) (:184-191); SH = H H^T (:200); stability check (:253-282).
@@ -704,31 +757,34 @@ __device__ __forceinline__ void ahtw_map(int item, int npanels, int ngt, int& p,
 // GTG: genes per tile (128 at full load; 64 for small grids: half the MFMA chain per wave, twice the
 // workgroups).  ngt = m_pad / GTG; npanels is a multiple of NPT.  Every shape accumulates in the
 // canonical GTile K order.
-template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1>
-static __global__ __launch_bounds__(256 * NPT,
-                                    (GTile<64 * NPT, GTG, NPT, 4, NBUF>::LDS_BYTES + NPT * PANEL * KMAX * 8 <= 81920)
-                                        ? 2 * NPT
-                                        : NPT)
+// PR = 16 is the narrow (tail) form: only the first 16 columns of panel 0 are live, so the tile covers
+// those 16 rows (WC waves along the genes): a quarter of the H / W bytes and MFMA work per gene tile.
+template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4>
+static __global__ __launch_bounds__(64 * NPT * WC,
+                                    (GTile<PR * NPT, GTG, NPT, WC, NBUF>::LDS_BYTES + NPT * PR * KMAX * 8 <= 81920)
+                                        ? 2 * NPT * WC / 4
+                                        : NPT * WC / 4)
 void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* __restrict__ Arm, long m_pad,
              double* __restrict__ W, const double* __restrict__ SHP, const ColInfo* __restrict__ ci,
              const int* __restrict__ colact, int npanels, int ngt) {
-  using TileW4 = GTile<64 * NPT, GTG, NPT, 4, NBUF>;
+  using TileW4 = GTile<PR * NPT, GTG, NPT, WC, NBUF>;
   constexpr int AHTW4_SH = TileW4::LDS_BYTES;
-  constexpr int AHTW4_LDS = AHTW4_SH + NPT * PANEL * KMAX * 8;
+  constexpr int AHTW4_LDS = AHTW4_SH + NPT * PR * KMAX * 8;
   static_assert(AHTW4_LDS <= 163840, "LDS of one CU");
-  constexpr int NTH = 256 * NPT;
+  static_assert(PR == PANEL || NPT == 1, "narrow tiles cover one panel");
+  constexpr int NTH = 64 * NPT * WC;
   __shared__ __attribute__((aligned(1024))) char smem[AHTW4_LDS];
   double* SHl = reinterpret_cast<double*>(smem + AHTW4_SH);
   int pp, gt;
   ahtw_map(xcd_item(blockIdx.x, (npanels / NPT) * ngt), npanels / NPT, ngt, pp, gt);
   const int p0 = pp * NPT;   // first panel of the tile
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w / WC, wc = w % WC;
   const int p = p0 + wr;     // this wave's panel
   ColInfo cc;
   uint64_t actmask = 0;
   TileW4 tl;
   tl.zero();
-  const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / 4) * wc + (lane & 15);
+  const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / WC) * wc + (lane & 15);
   double w0[TileW4::MB][TileW4::NB][4];
   const bool live = tl.template run<TileW4::MB * TileW4::NB * 4>(
       H + (long)p0 * PANEL * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
@@ -738,7 +794,8 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
 #pragma unroll
         for (int q = 0; q < NPT; ++q) ca[q] = colact[(long)(p0 + q) * PANEL + lane];
         const d2* src = reinterpret_cast<const d2*>(SHP + (long)p0 * PANEL * KMAX);
-        constexpr int NSH = NPT * PANEL * KMAX / 2 / NTH;
+        constexpr int NSH = NPT * PR * KMAX / 2 / NTH;
+        static_assert(NSH * 2 * NTH == NPT * PR * KMAX, "h h^T rows split evenly over the threads");
         d2 shv[NSH];
 #pragma unroll
         for (int j = 0; j < NSH; ++j) shv[j] = src[tid + NTH * j];
@@ -768,8 +825,8 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
       });
   if (!live) return;
   if (actmask == 0) return;   // this wave's panel is idle (its partner panel is not)
-  double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / 4) * wc + (lane & 15);
-  const double* SHw = SHl + (long)wr * PANEL * KMAX;
+  double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / WC) * wc + (lane & 15);
+  const double* SHw = SHl + (long)wr * PR * KMAX;
 #pragma unroll
   for (int mb = 0; mb < TileW4::MB; ++mb) {
     const int ra = 16 * mb + (lane & 15);
@@ -787,7 +844,7 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
 #pragma unroll
     for (int nb = 0; nb < TileW4::NB; ++nb) e[nb] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < 4 * TileW4::MB; ++q) {   // K = the tile's rows (restarts never leave the tile)
       if (4 * q + 3 < lo || 4 * q >= hi) continue;   // wave-uniform
       const int bb = 4 * q + (lane >> 4) - alc;
       const double av = (bb >= 0 && bb < ak) ? SHw[ra * KMAX + bb] : 0.0;

@@ -303,3 +303,27 @@ def test_c2_sweep_vs_reference(golden_c2, rule, key):
         assert np.array_equal(r.consensus[i], g[f"c2_counts_{key}_k{k}"] / R)
         for q, j in enumerate(g[f"c2_Hjobs_k{k}"]):
             assert relfro(r.H[j], g[f"c2_H_k{k}"][q]) < TOL
+
+
+@pytest.mark.parametrize("m,n,ks,R", [(1000, 40, [2, 3, 5], 1), (3001, 150, [7, 9], 1), (97, 33, [5], 2),
+                                      (2500, 300, [16], 1)])
+def test_narrow_end_kernels_bit_identical(oracle, golden, m, n, ks, R):
+    """The narrow end-of-sweep kernels (every restart inside columns 0..15 of panel 0) accumulate in the same
+    canonical K order as the 64-row tiles: W/H bit-identical with them disabled (NMFC_NARROW=0)."""
+    import os
+    from nmfconsensus_amd.nmf import Engine
+    A = golden["A_gct"] if (m, n) == (1000, 40) else np.asfortranarray(np.random.default_rng(m + n).random((m, n)))
+    runs = []
+    try:
+        for flag in ("1", "0"):
+            os.environ["NMFC_NARROW"] = flag
+            with Engine(A) as eng:
+                runs.append(eng.run(ks, R, maxiter=14, seed=3, stop_rule=0, want_factors=True))
+    finally:
+        os.environ.pop("NMFC_NARROW", None)
+    for j in range(len(ks) * R):
+        assert np.array_equal(runs[0].W[j], runs[1].W[j]) and np.array_equal(runs[0].H[j], runs[1].H[j]), j
+    k = ks[0]
+    W0, H0 = oracle.init_restart(3, m, n, k)
+    Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, 14, 0)
+    assert relfro(runs[0].W[0], Wo) < TOL and relfro(runs[0].H[0], Ho) < TOL

@@ -121,15 +121,17 @@ int main(int argc, char** argv) {
   const long g_ld = n_cols_pad;
   const int reps = 20;
   for (int live : lives) {
-    live = std::min(live, total_panels);
+    // live < 0: only the first -live restarts of panel 0 run (the end of a sweep: narrow forms apply)
+    const int only = live < 0 ? -live : 0;
+    live = live < 0 ? 1 : std::min(live, total_panels);
     const int npanels = (live + 3) / 4 * 4;
-    const int nlive = pfirst[live];   // restarts in the live panels
+    const int nlive = only ? only : pfirst[live];   // restarts still running
     std::vector<ColInfo> ci((size_t)npanels * PANEL, ColInfo{0, 0, 0, 0});
     std::vector<int> prb(npanels), pre(npanels), ca((size_t)npanels * PANEL, 0), st(nall, 1);
     double useful = 0;
     for (int p = 0; p < npanels; ++p) {
       prb[p] = p < live ? pfirst[p] : nlive;
-      pre[p] = p < live ? pfirst[p + 1] : nlive;
+      pre[p] = p < live ? std::min(pfirst[p + 1], nlive) : nlive;
     }
     for (int q = 0; q < nlive; ++q) {
       const RestartInfo& r = ri[q];
@@ -185,6 +187,21 @@ int main(int argc, char** argv) {
                hipLaunchKernelGGL((k_wta2<4, 128, 4, 2, 1, 3>), dim3(nsplit * ng * ntw), dim3(512), 0, 0, WTA_ARGS);
              }, reps));
     }
+    if (only && ri[nlive - 1].col0 + ri[nlive - 1].k <= 16) {   // narrow forms: live columns 0..15
+      const int ntq = (int)(n_cols_pad / 16);
+      report("wta narrow 16x16 nbuf4", timeit([&] {
+               hipLaunchKernelGGL((k_wta_narrow<16, 4>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
+                                  kchunk, dci, Gpart, g_ld, g_split, SWpart, sw_total);
+             }, reps));
+      report("wta narrow 16x16 nbuf8", timeit([&] {
+               hipLaunchKernelGGL((k_wta_narrow<16, 8>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
+                                  kchunk, dci, Gpart, g_ld, g_split, SWpart, sw_total);
+             }, reps));
+      report("wta narrow 16x32 nbuf6", timeit([&] {
+               hipLaunchKernelGGL((k_wta_narrow<32, 6>), dim3(nsplit * ntq / 2), dim3(64), 0, 0, W, Acm, m_pad, ntq / 2,
+                                  nsplit, kchunk, dci, Gpart, g_ld, g_split, SWpart, sw_total);
+             }, reps));
+    }
     report("hupdate", timeit([&] {
              hipLaunchKernelGGL(k_hupdate, dim3(nlive), dim3(NTH), 0, 0, 1, 1000000, STOP_FIXED, dri, n, n_pad, Gpart,
                                 g_ld, g_split, nsplit, SWpart, sw_total, Hh, SH, stop, reason, unch, cls, (long)512, nst,
@@ -207,6 +224,20 @@ int main(int argc, char** argv) {
     report("ahtw4 128 nbuf4", timeit([&] {
              hipLaunchKernelGGL((k_ahtw4<0, 128, 4>), dim3(npanels * ngt), dim3(256), 0, 0, AHTW_ARGS(ngt));
            }, reps));
+    if (only && ri[nlive - 1].col0 + ri[nlive - 1].k <= 16) {
+      report("ahtw narrow 16x64 (2w)", timeit([&] {
+               hipLaunchKernelGGL((k_ahtw4<0, 64, 3, 1, 16, 2>), dim3(2 * ngt), dim3(128), 0, 0, 1, Hh, n_pad, Arm,
+                                  m_pad, W, SHP, dci, colact, 1, 2 * ngt);
+             }, reps));
+      report("ahtw narrow 16x32 (2w)", timeit([&] {
+               hipLaunchKernelGGL((k_ahtw4<0, 32, 3, 1, 16, 2>), dim3(4 * ngt), dim3(128), 0, 0, 1, Hh, n_pad, Arm,
+                                  m_pad, W, SHP, dci, colact, 1, 4 * ngt);
+             }, reps));
+      report("ahtw narrow 16x128 (2w)", timeit([&] {
+               hipLaunchKernelGGL((k_ahtw4<0, 128, 3, 1, 16, 2>), dim3(ngt), dim3(128), 0, 0, 1, Hh, n_pad, Arm,
+                                  m_pad, W, SHP, dci, colact, 1, ngt);
+             }, reps));
+    }
     report("ahtw4 2x128 nbuf3 (8w)", timeit([&] {
              hipLaunchKernelGGL((k_ahtw4<0, 128, 3, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
            }, reps));
