@@ -215,7 +215,7 @@ def main():
     iters_all = []
     # per kernel id: [launches, ms, flop*launches, design bytes*launches, algorithmic bytes*launches]
     acc = {kid: [0, 0.0, 0.0, 0.0, 0.0] for kid in (_lib.KID_WTA, _lib.KID_AHTW, _lib.KID_HUPD, _lib.KID_LABELS,
-                                                     _lib.KID_COUNTS)}
+                                                     _lib.KID_COUNTS, _lib.KID_SMALL)}
     last = None
     for _ in range(args.steps):
         res, rho = step()
@@ -251,10 +251,10 @@ def main():
         f"step {elapsed / args.steps:.3f} s, engine {res.seconds_total:.3f} s (iterate {res.seconds_iterate:.3f} s)")
 
     roof = None
-    if timing and acc[_lib.KID_WTA][0] and acc[_lib.KID_AHTW][0]:
+    if timing and ((acc[_lib.KID_WTA][0] and acc[_lib.KID_AHTW][0]) or acc[_lib.KID_SMALL][0]):
         kernels = {}
         names = {_lib.KID_WTA: "wta", _lib.KID_AHTW: "ahtw", _lib.KID_HUPD: "hupdate", _lib.KID_LABELS: "labels",
-                 _lib.KID_COUNTS: "counts"}
+                 _lib.KID_COUNTS: "counts", _lib.KID_SMALL: "small_mu"}
         for kid, (c, ms, fl, b, ab) in acc.items():
             if not c:
                 continue
@@ -273,7 +273,8 @@ def main():
             kernels[names[kid]] = kr
         if rank == 0:
             kernels.update(side_kernels(A_dev, m, n, max(ks)))
-        dom = max(("wta", "ahtw"), key=lambda s: kernels[s]["avg_ms"] * kernels[s]["launches"])
+        dom = max([x for x in ("wta", "ahtw", "small_mu") if x in kernels],
+                  key=lambda s: kernels[s]["avg_ms"] * kernels[s]["launches"])
         ach = kernels[dom]["tflops"]
         roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None,

@@ -168,7 +168,8 @@ const char* nmfc_version(void);
 /* Per-kernel device time (ms) accumulated over the last run, measured with HIP events on the
  * engine's stream: kernel ids 0 = wta (W^T A + W^T W, MFMA), 1 = hupdate (H update + stop check),
  * 2 = ahtw (A h^T MFMA + W update), 3 = init, 4 = other (repack moves, TolX W check), 5 = labels,
- * 6 = connectivity counts.  Returns the number of launches of that kernel. */
+ * 6 = connectivity counts, 7 = small-shape persistent MU kernel (m_pad <= 1024, n <= 64: the whole
+ * loop in one launch).  Returns the number of launches of that kernel. */
 long long nmfc_engine_kernel_time(nmfc_engine* e, int kernel_id, double* ms_out);
 /* Enables per-launch event timing (adds small overhead; used by bench.py's roofline leg). */
 void nmfc_engine_set_timing(nmfc_engine* e, int enable);

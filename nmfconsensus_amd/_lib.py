@@ -18,7 +18,7 @@ c_int = ctypes.c_int
 STOP_FIXED, STOP_REF_COMPAT, STOP_ARGMAX_STABLE, STOP_TOLX = 0, 1, 2, 3
 LABEL_ARGMAX, LABEL_R_ORDER = 0, 1
 INIT_LIBNMF, INIT_R_RUNIF = 0, 1
-KID_WTA, KID_HUPD, KID_AHTW, KID_INIT, KID_OTHER, KID_LABELS, KID_COUNTS = 0, 1, 2, 3, 4, 5, 6
+KID_WTA, KID_HUPD, KID_AHTW, KID_INIT, KID_OTHER, KID_LABELS, KID_COUNTS, KID_SMALL = 0, 1, 2, 3, 4, 5, 6, 7
 
 
 class SweepOpts(ctypes.Structure):

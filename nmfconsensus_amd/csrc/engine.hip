@@ -115,7 +115,7 @@ std::vector<uint32_t> make_jump_table(int nchunks) {
   return table;
 }
 
-enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID_LABELS = 5, KID_COUNTS = 6, KID_N = 7 };
+enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID_LABELS = 5, KID_COUNTS = 6, KID_SMALL = 7, KID_N = 8 };
 
 // Packing of a restart list into 64-column panels by first-fit decreasing (k descending, ties by rid;
 // a restart never straddles a panel), so the k = 10 / 6 / 5 panels' spare columns take small-k
@@ -180,6 +180,42 @@ bool narrow_packing(const Packing& pk) {
   return true;
 }
 
+// Small-shape path (k_small_mu): restarts packed first-fit decreasing into 16-column blocks (a restart never
+// straddles a block, at most SMALL_MAXR per block); the Packing's panels only size the stacked buffers.
+Packing pack_small(const std::vector<RestartInfo>& in, std::vector<SmallBlock>& blocks) {
+  std::vector<RestartInfo> srt(in);
+  std::stable_sort(srt.begin(), srt.end(), [](const RestartInfo& a, const RestartInfo& b) {
+    return a.k != b.k ? a.k > b.k : a.rid < b.rid;
+  });
+  std::vector<int> fill;
+  blocks.clear();
+  Packing pk;
+  for (RestartInfo r : srt) {
+    size_t b = 0;
+    while (b < fill.size() && (fill[b] + r.k > 16 || blocks[b].nr == SMALL_MAXR)) ++b;
+    if (b == fill.size()) {
+      fill.push_back(0);
+      SmallBlock sb{};
+      sb.col0 = (int)b * 16;
+      blocks.push_back(sb);
+    }
+    SmallBlock& sb = blocks[b];
+    r.col0 = sb.col0 + fill[b];
+    sb.rid[sb.nr] = r.rid;
+    sb.k[sb.nr] = r.k;
+    sb.lc0[sb.nr] = fill[b];
+    ++sb.nr;
+    fill[b] += r.k;
+    pk.ri.push_back(r);
+  }
+  pk.npanels = std::max(1, (int)((blocks.size() * 16 + PANEL - 1) / PANEL));
+  while (pk.npanels % WTA_NPT) ++pk.npanels;
+  pk.prb.assign(pk.npanels, 0);
+  pk.pre.assign(pk.npanels, 0);
+  pk.ci.assign((size_t)pk.npanels * PANEL, ColInfo{0, 0, 0, 0});
+  return pk;
+}
+
 // panels holding at least one restart (the packing fills panels from 0; the rest pad the 4-panel groups)
 int live_panels(const Packing& pk) {
   int np = 0;
@@ -203,12 +239,13 @@ struct nmfc_engine {
   int force_wta = -1, force_ahtw = -1;   // tile-shape overrides (env NMFC_WTA_TILE / NMFC_AHTW_TILE)
   int repack_div = 5;                     // repack after nact / repack_div stops (env NMFC_REPACK_DIV)
   bool narrow_ok = true;                  // narrow end-of-sweep kernels allowed (env NMFC_NARROW=0 disables)
+  bool small_ok = true;                   // small-shape persistent kernel allowed (env NMFC_SMALL=0 disables)
   DevBuf Acm, Arm;
   // per-run buffers (grow-only)
   DevBuf W[2], H[2], Gpart, SWpart, SH, SHP, colact, Hfin, Wfin;
   DevBuf rinfo, stop_iter, stop_reason, unchanged, classes, n_stopped, Hstat, Wsnap;
   DevBuf prb, pre, colinfo, moves, finfo;
-  DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp;
+  DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp, smallblk;
   int jump_chunks = 0;
   int* h_stopped = nullptr;   // pinned, 2 slots
   // timing
@@ -268,6 +305,45 @@ TileChoice choose_tiles(const nmfc_engine* e, int np_live, int ntj) {
   if (e->force_wta >= 0) tc.wta = e->force_wta;   // NMFC_WTA_TILE (tests: every shape gives the same bits)
   if (e->force_ahtw >= 0) tc.ahtw_small = e->force_ahtw == 1;
   return tc;
+}
+
+// k_small_mu<GBW, JB> for this engine's shape (GBW = m_pad / 64 gene blocks per wave, JB = sample blocks)
+template <int GBW>
+hipError_t launch_small_g(nmfc_engine* e, int nblocks, int maxiter, int stop_rule) {
+  const int jb = (e->n + 15) / 16;
+  auto args = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * SMALL_NW), 0, e->st, e->smallblk.as<SmallBlock>(),
+                       e->Arm.as<double>(), e->n_pad, e->Acm.as<double>(), e->m_pad, e->n, e->n_pad,
+                       e->W[0].as<double>(), e->H[0].as<double>(), maxiter, stop_rule, e->stop_iter.as<int>(),
+                       e->stop_reason.as<int>());
+  };
+  switch (jb) {
+    case 1: args(k_small_mu<GBW, 1>); break;
+    case 2: args(k_small_mu<GBW, 2>); break;
+    case 3: args(k_small_mu<GBW, 3>); break;
+    default: args(k_small_mu<GBW, 4>); break;
+  }
+  return hipGetLastError();
+}
+
+int launch_small(nmfc_engine* e, int nblocks, int maxiter, int stop_rule) {
+  hipError_t err;
+  switch (e->m_pad / 64) {
+    case 2: err = launch_small_g<2>(e, nblocks, maxiter, stop_rule); break;
+    case 4: err = launch_small_g<4>(e, nblocks, maxiter, stop_rule); break;
+    case 6: err = launch_small_g<6>(e, nblocks, maxiter, stop_rule); break;
+    case 8: err = launch_small_g<8>(e, nblocks, maxiter, stop_rule); break;
+    case 10: err = launch_small_g<10>(e, nblocks, maxiter, stop_rule); break;
+    case 12: err = launch_small_g<12>(e, nblocks, maxiter, stop_rule); break;
+    case 14: err = launch_small_g<14>(e, nblocks, maxiter, stop_rule); break;
+    case 16: err = launch_small_g<16>(e, nblocks, maxiter, stop_rule); break;
+    default: set_err("k_small_mu: m_pad %ld unsupported", e->m_pad); return -1;
+  }
+  if (err != hipSuccess) {
+    set_err("k_small_mu launch: %s", hipGetErrorString(err));
+    return -1;
+  }
+  return 0;
 }
 
 hipEvent_t take_event(nmfc_engine* e) {
@@ -367,6 +443,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   }
   if (const char* s = getenv("NMFC_REPACK_DIV")) e->repack_div = std::max(1, atoi(s));
   if (const char* s = getenv("NMFC_NARROW")) e->narrow_ok = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_SMALL")) e->small_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
     const std::string v(s);
     e->force_ahtw = v == "128" ? 0 : v == "64" ? 1 : -1;
@@ -419,7 +496,7 @@ void nmfc_engine_destroy(nmfc_engine* e) {
                     &e->stop_iter, &e->stop_reason, &e->unchanged, &e->classes, &e->n_stopped, &e->prb,
                     &e->pre,       &e->colinfo,   &e->moves,     &e->finfo,     &e->initjobs, &e->chunk_job,  &e->chunk_idx,
                     &e->jump,      &e->labels,    &e->slot,      &e->grp_begin, &e->grp_list,  &e->counts_tmp,
-                    &e->cons_tmp,  &e->Hstat,     &e->Wsnap};
+                    &e->cons_tmp,  &e->Hstat,     &e->Wsnap,     &e->smallblk};
   for (DevBuf* b : bufs) b->release();
   if (e->h_stopped) (void)hipHostFree(e->h_stopped);
   if (e->st) (void)hipStreamDestroy(e->st);
@@ -514,7 +591,11 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     sw_total += (long)all[rid].k * all[rid].k;
     hoff[rid + 1] = hoff[rid] + all[rid].k;
   }
-  Packing pk = pack(all);
+  // small shapes: one persistent workgroup per 16-column block runs the whole loop (a function of m, n and
+  // the stop rule only, so a job takes the same path -- and gives the same bits -- in any batch)
+  const bool small = e->small_ok && e->m_pad <= 1024 && n <= 64 && opts.stop_rule != NMFC_STOP_TOLX;
+  std::vector<SmallBlock> sblocks;
+  Packing pk = small ? pack_small(all, sblocks) : pack(all);
   const long cap_cols = (long)pk.npanels * PANEL;
   const int ntj = (int)(e->n_cols_pad / 128);
   const long g_ld = e->n_cols_pad;
@@ -664,6 +745,17 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   // ---- iterate ----
   auto t_iter0 = std::chrono::steady_clock::now();
   int it = 0, q = 0, checked = 0;
+  if (small) {
+    if (e->smallblk.ensure(sizeof(SmallBlock) * sblocks.size())) return -1;
+    HCHECK(hipMemcpyAsync(e->smallblk.p, sblocks.data(), sizeof(SmallBlock) * sblocks.size(), hipMemcpyHostToDevice, st));
+    {
+      TimedLaunch tl(e, KID_SMALL);
+      if (launch_small(e, (int)sblocks.size(), opts.maxiter, opts.stop_rule)) return -1;
+    }
+    HCHECK(hipStreamSynchronize(st));
+    if (e->timing) drain_timing(e);
+    it = opts.maxiter;   // every restart records its own stop iteration
+  }
   int nact = nj;
   int stopped_at_pack = 0;
   struct PollEvents {   // destroyed on every exit path, including HCHECK returns
@@ -677,7 +769,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   HCHECK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
   HCHECK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
   std::vector<int> si(nj);
-  for (;;) {
+  for (; !small;) {
     if (it < opts.maxiter) {
       const int chunk = std::min(opts.check_every, opts.maxiter - it);
       // tile shapes by grid size (a speed choice only: every shape sums in the canonical K order)
@@ -929,6 +1021,11 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     e->kflops[KID_AHTW] = fl_ahtw / c;
     e->kbytes_algo[KID_AHTW] = a_bytes + ba_ahtw / c;
     e->kbytes[KID_AHTW] = a_bytes + b_ahtw / c;
+  }
+  if (const long long c = e->kcount[KID_SMALL]) {   // the whole MU iteration in one persistent launch
+    e->kflops[KID_SMALL] = (fl_wta + fl_ahtw) / c;
+    e->kbytes_algo[KID_SMALL] = (ba_wta + ba_ahtw + ba_hupd) / c;
+    e->kbytes[KID_SMALL] = e->kbytes_algo[KID_SMALL];
   }
   if (const long long c = e->kcount[KID_HUPD]) {
     e->kbytes_algo[KID_HUPD] = ba_hupd / c;

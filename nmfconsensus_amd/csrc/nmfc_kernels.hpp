@@ -866,6 +866,269 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
 }
 
 // ---------------------------------------------------------------------------------------------
+// Small shapes (m_pad <= 1024, n <= 64: the bundled gct, BASELINE configs[0..1]): ONE persistent workgroup
+// runs a 16-column block of restarts (restarts never straddle a block) through the whole MU loop and the
+// stop rule in-kernel -- no per-iteration launches, A read from L2.  4 waves; wave w owns the gene blocks
+// [w*GBW, (w+1)*GBW) and keeps its W rows in registers in the fp64 MFMA D layout
+//   w[gb][r] = W[g = 16*(w*GBW + gb) + (lane>>4) + 4r][c = lane & 15],
+// which is at once the A operand of G = W^T A and of W^T W (K = genes), and the D layout of
+// F = A h^T, E = W0 (h h^T) and the W update, so W never moves.  Per iteration (nmf_mu.c:174-216):
+//   G, W^T W   per wave over its genes (MFMA chains in gene order), the 4 wave partials summed in wave order
+//   H update   h = mu_rule(H, G, (W^T W) H) per (column, sample), d summed over the restart's columns in order
+//   h h^T      one wave, MFMA over the samples (zeroed across restarts)
+//   F, E, W    per wave: F = A h^T (K = samples), E = W0 (h h^T) (W0 transposed through LDS), W rule
+//   stop rule  every even iteration (REF_COMPAT windows / ARGMAX_STABLE classes), nmf_mu.c:253-282
+// A restart that stops freezes its columns; the block ends when all its restarts have stopped.
+// Deterministic: every reduction order is a function of (m, n) only, so a job gives the same bits in
+// any block and any batch.
+// ---------------------------------------------------------------------------------------------
+constexpr int SMALL_NW = 4;
+constexpr int SMALL_MAXR = 8;   // restarts per 16-column block (k >= 2)
+
+struct SmallBlock {
+  int col0;                  // first stacked column of the block (W/H rows col0 .. col0 + 15)
+  int nr;                    // restarts in the block
+  int rid[SMALL_MAXR];       // persistent restart ids
+  int k[SMALL_MAXR];
+  int lc0[SMALL_MAXR];       // block-local first column
+};
+
+template <int JB>
+struct SmallSmem {
+  double H[16][16 * JB];           // current H of the block (rows = columns c)
+  double Gp[SMALL_NW][16][16 * JB];
+  double SWp[SMALL_NW][16][16];
+  double SW[16][16];
+  double S[16][16];                // h h^T, zero across restarts
+  double T[SMALL_NW][16][17];      // per-wave W0 block transposition (padded rows)
+  double win[SMALL_MAXR][16][16];  // REF_COMPAT windows
+  int cls[SMALL_MAXR][64];         // classes (REF_COMPAT: windows i < k; ARGMAX_STABLE: samples)
+  int colr[16];                    // restart slot of each column (-1: padding)
+  int run[SMALL_MAXR];             // 1 while the restart runs
+  int unch[SMALL_MAXR];
+  int changed[SMALL_MAXR];
+  int nrun;
+};
+
+template <int GBW, int JB>
+static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
+    const SmallBlock* __restrict__ blocks, const double* __restrict__ Arm, long ld_rm, const double* __restrict__ Acm,
+    long m_pad, int n, long n_pad, double* __restrict__ W, double* __restrict__ H, int maxiter, int stop_rule,
+    int* __restrict__ stop_iter, int* __restrict__ stop_reason) {
+  constexpr int NP = 16 * JB;
+  __shared__ SmallSmem<JB> sm;
+  __shared__ SmallBlock blk;   // in LDS: indexed by restart slot at run time
+  if (threadIdx.x == 0) blk = blocks[blockIdx.x];
+  __syncthreads();
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, lr = l >> 4, lc = l & 15;
+  const int nr = blk.nr;
+  // ---- state ----
+  if (tid < 16) sm.colr[tid] = -1;
+  __syncthreads();
+  if (tid < nr)
+    for (int a = 0; a < blk.k[tid]; ++a) sm.colr[blk.lc0[tid] + a] = tid;
+  if (tid < SMALL_MAXR) {
+    sm.run[tid] = tid < nr;
+    sm.unch[tid] = 0;
+  }
+  for (int x = tid; x < SMALL_MAXR * 64; x += 64 * SMALL_NW) (&sm.cls[0][0])[x] = 0;   // nmf_mu.c:132
+  for (int x = tid; x < 16 * NP; x += 64 * SMALL_NW) {
+    const int c = x / NP, j = x % NP;
+    sm.H[c][j] = (j < n) ? H[(long)(blk.col0 + c) * n_pad + j] : 0.0;
+  }
+  double wr[GBW][4];
+#pragma unroll
+  for (int gb = 0; gb < GBW; ++gb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      wr[gb][r] = W[(long)(blk.col0 + lc) * m_pad + 16 * (w * GBW + gb) + 4 * r + lr];
+  if (tid == 0) sm.nrun = nr;
+  __syncthreads();
+  for (int iter = 1; iter <= maxiter; ++iter) {
+    // the operand base pointers are laundered every iteration: otherwise the compiler hoists the
+    // per-k-step addresses of all 4*GBW k-steps out of the iteration loop (hundreds of registers)
+    const double* ArmI = Arm;
+    const double* AcmI = Acm;
+    asm volatile("" : "+s"(ArmI), "+s"(AcmI));
+    // ---- G = W^T A, W^T W over this wave's genes ----
+    d4 gacc[JB], sacc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int jb = 0; jb < JB; ++jb) gacc[jb] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int gb = 0; gb < GBW; ++gb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long g = 16 * (w * GBW + gb) + 4 * r + lr;
+        double av[JB];
+#pragma unroll
+        for (int jb = 0; jb < JB; ++jb) av[jb] = ArmI[g * ld_rm + 16 * jb + lc];
+#pragma unroll
+        for (int jb = 0; jb < JB; ++jb) gacc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(wr[gb][r], av[jb], gacc[jb], 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(wr[gb][r], wr[gb][r], sacc, 0, 0, 0);
+        if (r == 1 || r == 3) __builtin_amdgcn_sched_barrier(0);   // loads at most 2 k-steps ahead
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int jb = 0; jb < JB; ++jb) sm.Gp[w][lr + 4 * r][16 * jb + lc] = gacc[jb][r];
+      sm.SWp[w][lr + 4 * r][lc] = sacc[r];
+    }
+    __syncthreads();
+    {   // W^T W: wave partials in wave order
+      const int c = tid >> 4, d = tid & 15;
+      sm.SW[c][d] = ((sm.SWp[0][c][d] + sm.SWp[1][c][d]) + sm.SWp[2][c][d]) + sm.SWp[3][c][d];
+      if (tid < SMALL_MAXR) sm.changed[tid] = 0;
+    }
+    __syncthreads();
+    // ---- H update (nmf_mu.c:178, 184-191), new H kept in registers until every thread has read the old ----
+    double hn[(16 * NP + 64 * SMALL_NW - 1) / (64 * SMALL_NW)];
+#pragma unroll
+    for (int u = 0; u < (16 * NP + 64 * SMALL_NW - 1) / (64 * SMALL_NW); ++u) {
+      const int x = tid + u * 64 * SMALL_NW;
+      hn[u] = 0.0;
+      if (x < 16 * NP) {
+        const int c = x / NP, j = x % NP;
+        const int q = sm.colr[c];
+        const double h0 = sm.H[c][j];
+        hn[u] = h0;
+        if (q >= 0 && sm.run[q] && j < n) {
+          const double gsum = ((sm.Gp[0][c][j] + sm.Gp[1][c][j]) + sm.Gp[2][c][j]) + sm.Gp[3][c][j];
+          const int b0 = blk.lc0[q], kq = blk.k[q];
+          double dsum = 0.0;
+          for (int b = 0; b < kq; ++b) dsum = fma(sm.SW[c][b0 + b], sm.H[b0 + b][j], dsum);
+          hn[u] = mu_rule(h0, gsum, dsum);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < (16 * NP + 64 * SMALL_NW - 1) / (64 * SMALL_NW); ++u) {
+      const int x = tid + u * 64 * SMALL_NW;
+      if (x < 16 * NP) sm.H[x / NP][x % NP] = hn[u];
+    }
+    __syncthreads();
+    // ---- h h^T (nmf_mu.c:200) by wave 0; stop rule (nmf_mu.c:253-282) by the other waves ----
+    const bool check = stop_rule != STOP_FIXED && iter > 1 && (iter % 2 == 0);
+    if (w == 0) {
+      d4 hh = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < NP / 4; ++q) {
+        const double hv = sm.H[lc][4 * q + lr];
+        hh = __builtin_amdgcn_mfma_f64_16x16x4f64(hv, hv, hh, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = lr + 4 * r, d = lc;
+        const int qc = sm.colr[c];
+        sm.S[c][d] = (qc >= 0 && qc == sm.colr[d]) ? hh[r] : 0.0;
+      }
+    }
+    __syncthreads();
+    if (check) {
+      if (stop_rule == STOP_REF_COMPAT) {
+        // window i of restart q reads the flat k x n column-major buffer at [i*n, i*n + k)
+        for (int x = tid; x < nr * 16; x += 64 * SMALL_NW) {
+          const int q = x >> 4, i = x & 15, kq = blk.k[q];
+          if (i >= kq || i >= n || !sm.run[q]) continue;
+          int cl = 0;
+          double prev = 0.0;
+          for (int jj = 0; jj < kq; ++jj) {
+            const int f = i * n + jj, j = f / kq, a = f - j * kq;
+            const double v = sm.H[blk.lc0[q] + a][j];
+            if (jj > 0 && v > prev) cl = jj;
+            prev = v;
+          }
+          if (sm.cls[q][i] != cl) {
+            sm.cls[q][i] = cl;
+            sm.changed[q] = 1;
+          }
+        }
+      } else if (stop_rule == STOP_ARGMAX_STABLE) {
+        for (int x = tid; x < nr * 64; x += 64 * SMALL_NW) {
+          const int q = x >> 6, j = x & 63;
+          if (j >= n || !sm.run[q]) continue;
+          int best = 0;
+          double bv = sm.H[blk.lc0[q]][j];
+          for (int a = 1; a < blk.k[q]; ++a) {
+            const double v = sm.H[blk.lc0[q] + a][j];
+            if (v > bv) {
+              bv = v;
+              best = a;
+            }
+          }
+          if (sm.cls[q][j] != best) {
+            sm.cls[q][j] = best;
+            sm.changed[q] = 1;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- F = A h^T, E = W0 (h h^T), W update (nmf_mu.c:198-216) ----
+    int runmask = 0;
+#pragma unroll
+    for (int q = 0; q < SMALL_MAXR; ++q) runmask |= (q < nr && sm.run[q]) ? (1 << q) : 0;
+    const int qmine = sm.colr[lc];
+    const bool upd = qmine >= 0 && ((runmask >> qmine) & 1);
+#pragma unroll
+    for (int gb = 0; gb < GBW; ++gb) {
+      const long g0 = 16 * (w * GBW + gb);
+      d4 f = (d4){0.0, 0.0, 0.0, 0.0}, e = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < NP / 4; ++q) {
+        const double av = AcmI[(long)(4 * q + lr) * m_pad + g0 + lc];
+        f = __builtin_amdgcn_mfma_f64_16x16x4f64(av, sm.H[lc][4 * q + lr], f, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sm.T[w][lr + 4 * r][lc] = wr[gb][r];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        e = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.T[w][lc][4 * q + lr], sm.S[4 * q + lr][lc], e, 0, 0, 0);
+      __builtin_amdgcn_wave_barrier();
+      if (upd) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wr[gb][r] = mu_rule(wr[gb][r], f[r], e[r]);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one gene block's loads in flight at a time
+    }
+    // ---- stop bookkeeping (one thread), then every thread sees the new run flags ----
+    if (tid == 0) {
+      for (int q = 0; q < nr; ++q) {
+        if (!sm.run[q]) continue;
+        int reason = 0;
+        if (check) {
+          if (!sm.changed[q]) {
+            if (++sm.unch[q] >= 200) reason = 1;   // nmf_mu.c:269-271
+          } else {
+            sm.unch[q] = 0;
+          }
+        }
+        if (!reason && iter >= maxiter) reason = 2;
+        if (reason) {
+          sm.run[q] = 0;
+          --sm.nrun;
+          stop_iter[blk.rid[q]] = iter;
+          stop_reason[blk.rid[q]] = reason;
+        }
+      }
+    }
+    __syncthreads();
+    if (sm.nrun == 0) break;
+  }
+  // ---- final factors back to the stacked layout ----
+#pragma unroll
+  for (int gb = 0; gb < GBW; ++gb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      W[(long)(blk.col0 + lc) * m_pad + 16 * (w * GBW + gb) + 4 * r + lr] = wr[gb][r];
+  for (int x = tid; x < 16 * NP; x += 64 * SMALL_NW) {
+    const int c = x / NP, j = x % NP;
+    if (j < n) H[(long)(blk.col0 + c) * n_pad + j] = sm.H[c][j];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Repacking (compaction of live restarts) and the final-factor archive: k rows per job.
 // ---------------------------------------------------------------------------------------------
 struct MoveJob {
