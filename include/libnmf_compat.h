@@ -50,6 +50,10 @@ typedef struct options_t {
  * runs on the GPU (HIP, gfx950).  Prints "Exiting nmf_mu after <iter>\n" like nmf_mu.c:296.
  * The stop rule is the reference's class-stability check (nmf_mu.c:253-282) in its defined
  * REF_COMPAT form.  Returns 0, or -1 on allocation / device failure (nmf_mu.c:138-151).
+ * Rank limit: 2 <= k <= min(16, m, n).  The reference accepts any k; this engine keeps each
+ * restart's k x k blocks in one 16-wide MFMA tile (KMAX, nmfconsensus_amd/csrc/nmfc_kernels.hpp), so
+ * k > 16 (and k = 1, which nmf.r:107-108 never passes) prints "Error in nmf_mu: nmfc_engine_run: k=<k> unsupported ..." to stderr before any
+ * device work, leaves w0/h0 untouched and returns -1.
  */
 double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int* maxiter,
               const double* pTolX, const double* pTolFun);

@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
+#include <cstring>
+#include <mutex>
 #include <algorithm>
 #include <vector>
 
@@ -105,6 +107,29 @@ void generateMatrix(const int* pm, const int* pn, const int* pk, init_t* pinit, 
   }
 }
 
+// The engine behind nmf_mu is kept across calls with the same A (nmf.r calls nmf_mu once per restart on
+// one data matrix, nmf.r:41-45; R passes a fresh copy each time, so A is matched by shape and content).
+// Creating an engine uploads A and builds its two layouts, and its first run allocates the work buffers:
+// on the gct shape that is several times the whole MU loop.  NMFC_NMF_MU_CACHE=0 disables the cache.
+namespace {
+std::mutex g_mu_lock;
+struct MuCache {
+  nmfc_engine* e = nullptr;
+  int m = 0, n = 0;
+  uint64_t hash = 0;   // no destructor: HIP may already be torn down when statics are destroyed at exit
+} g_mu;
+
+uint64_t hash_matrix(const double* a, size_t len) {   // FNV-1a over the bytes, 8 at a time
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < len; ++i) {
+    uint64_t v;
+    memcpy(&v, a + i, 8);
+    h = (h ^ v) * 1099511628211ull;
+  }
+  return h;
+}
+}  // namespace
+
 // nmf_mu.c:84-315 on the GPU engine
 double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int* maxiter, const double* pTolX,
               const double* pTolFun) {
@@ -115,7 +140,34 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
     printf("Exiting nmf_mu after %i\n", 1);
     return 0;
   }
-  nmfc_engine* e = nmfc_engine_create(-1, a, m, n, 0);
+  if (k < 2 || k > nmfc::KMAX || k > m || k > n) {   // checked before any device work (libnmf_compat.h)
+    fprintf(stderr, "Error in nmf_mu: nmfc_engine_run: k=%d unsupported (need 2 <= k <= min(%d, m, n))\n", k,
+            nmfc::KMAX);
+    return -1;
+  }
+  const char* cache_env = getenv("NMFC_NMF_MU_CACHE");
+  const bool cache = !(cache_env && atoi(cache_env) == 0);
+  std::unique_lock<std::mutex> lock(g_mu_lock, std::defer_lock);
+  nmfc_engine* e = nullptr;
+  if (cache) {
+    lock.lock();
+    const uint64_t h = hash_matrix(a, (size_t)m * n);
+    if (g_mu.e && g_mu.m == m && g_mu.n == n && g_mu.hash == h) {
+      e = g_mu.e;
+    } else {
+      nmfc_engine_destroy(g_mu.e);
+      g_mu.e = nullptr;
+      e = nmfc_engine_create(-1, a, m, n, 0);
+      if (e) {
+        g_mu.e = e;
+        g_mu.m = m;
+        g_mu.n = n;
+        g_mu.hash = h;
+      }
+    }
+  } else {
+    e = nmfc_engine_create(-1, a, m, n, 0);
+  }
   if (!e) {
     fprintf(stderr, "Error in nmf_mu: %s\n", nmfc_last_error());
     return -1;
@@ -133,7 +185,7 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
   r.H = h0;
   const int ks[1] = {k};
   int rc = nmfc_engine_run(e, ks, 1, 1, &o, w0, h0, &r);
-  nmfc_engine_destroy(e);
+  if (!cache) nmfc_engine_destroy(e);
   if (rc != 0) {
     fprintf(stderr, "Error in nmf_mu: %s\n", nmfc_last_error());
     return -1;

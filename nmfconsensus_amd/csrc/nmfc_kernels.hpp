@@ -884,6 +884,7 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
 // ---------------------------------------------------------------------------------------------
 constexpr int SMALL_NW = 4;
 constexpr int SMALL_MAXR = 8;   // restarts per 16-column block (k >= 2)
+constexpr int SMALL_GGMAX = 4;  // gene blocks per F/E group: 4 when GBW % 4 == 0, else 2 (GBW is even)
 
 struct SmallBlock {
   int col0;                  // first stacked column of the block (W/H rows col0 .. col0 + 15)
@@ -900,7 +901,7 @@ struct SmallSmem {
   double SWp[SMALL_NW][16][16];
   double SW[16][16];
   double S[16][16];                // h h^T, zero across restarts
-  double T[SMALL_NW][16][17];      // per-wave W0 block transposition (padded rows)
+  double T[SMALL_NW][SMALL_GGMAX][16][17];   // per-wave W0 block transpositions (padded rows), SMALL_GG blocks
   double win[SMALL_MAXR][16][16];  // REF_COMPAT windows
   int cls[SMALL_MAXR][64];         // classes (REF_COMPAT: windows i < k; ARGMAX_STABLE: samples)
   int colr[16];                    // restart slot of each column (-1: padding)
@@ -910,7 +911,9 @@ struct SmallSmem {
   int nrun;
 };
 
-template <int GBW, int JB>
+// SKIP != 0 only in tools/smallbench.hip (phase cost breakdown): bit 0 no G/W^T W, 1 no H update,
+// 2 no h h^T / stop rule, 3 no F/E/W update.
+template <int GBW, int JB, int SKIP = 0>
 static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     const SmallBlock* __restrict__ blocks, const double* __restrict__ Arm, long ld_rm, const double* __restrict__ Acm,
     long m_pad, int n, long n_pad, double* __restrict__ W, double* __restrict__ H, int maxiter, int stop_rule,
@@ -955,7 +958,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
 #pragma unroll
     for (int jb = 0; jb < JB; ++jb) gacc[jb] = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int gb = 0; gb < GBW; ++gb)
+    for (int gb = 0; gb < ((SKIP & 1) ? 0 : GBW); ++gb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const long g = 16 * (w * GBW + gb) + 4 * r + lr;
@@ -965,7 +968,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb) gacc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(wr[gb][r], av[jb], gacc[jb], 0, 0, 0);
         sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(wr[gb][r], wr[gb][r], sacc, 0, 0, 0);
-        if (r == 1 || r == 3) __builtin_amdgcn_sched_barrier(0);   // loads at most 2 k-steps ahead
+        if (r == 3 && (gb & 1)) __builtin_amdgcn_sched_barrier(0);   // loads at most 8 k-steps ahead
       }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -991,7 +994,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
         const int q = sm.colr[c];
         const double h0 = sm.H[c][j];
         hn[u] = h0;
-        if (q >= 0 && sm.run[q] && j < n) {
+        if (!(SKIP & 2) && q >= 0 && sm.run[q] && j < n) {
           const double gsum = ((sm.Gp[0][c][j] + sm.Gp[1][c][j]) + sm.Gp[2][c][j]) + sm.Gp[3][c][j];
           const int b0 = blk.lc0[q], kq = blk.k[q];
           double dsum = 0.0;
@@ -1008,8 +1011,8 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     }
     __syncthreads();
     // ---- h h^T (nmf_mu.c:200) by wave 0; stop rule (nmf_mu.c:253-282) by the other waves ----
-    const bool check = stop_rule != STOP_FIXED && iter > 1 && (iter % 2 == 0);
-    if (w == 0) {
+    const bool check = !(SKIP & 4) && stop_rule != STOP_FIXED && iter > 1 && (iter % 2 == 0);
+    if (w == 0 && !(SKIP & 4)) {
       d4 hh = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int q = 0; q < NP / 4; ++q) {
@@ -1070,27 +1073,46 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     for (int q = 0; q < SMALL_MAXR; ++q) runmask |= (q < nr && sm.run[q]) ? (1 << q) : 0;
     const int qmine = sm.colr[lc];
     const bool upd = qmine >= 0 && ((runmask >> qmine) & 1);
+    constexpr int SMALL_GG = (GBW % 4 == 0) ? 4 : 2;
+    const int nq = (n + 3) >> 2;
+    // GG gene blocks at a time: GG independent MFMA chains for F and for E (a single chain per block would
+    // leave the matrix pipe waiting on the dependent-issue latency)
 #pragma unroll
-    for (int gb = 0; gb < GBW; ++gb) {
-      const long g0 = 16 * (w * GBW + gb);
-      d4 f = (d4){0.0, 0.0, 0.0, 0.0}, e = (d4){0.0, 0.0, 0.0, 0.0};
+    for (int g4 = 0; g4 < ((SKIP & 8) ? 0 : GBW); g4 += SMALL_GG) {
+      d4 f[SMALL_GG], e[SMALL_GG];
 #pragma unroll
-      for (int q = 0; q < NP / 4; ++q) {
-        const double av = AcmI[(long)(4 * q + lr) * m_pad + g0 + lc];
-        f = __builtin_amdgcn_mfma_f64_16x16x4f64(av, sm.H[lc][4 * q + lr], f, 0, 0, 0);
+      for (int i = 0; i < SMALL_GG; ++i) {
+        f[i] = (d4){0.0, 0.0, 0.0, 0.0};
+        e[i] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm.T[w][i][lr + 4 * r][lc] = wr[g4 + i][r];
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sm.T[w][lr + 4 * r][lc] = wr[gb][r];
+      for (int q = 0; q < NP / 4; ++q) {
+        if (q >= nq) break;   // samples >= n: zero rows of h^T (dropping them leaves F bit-identical)
+        double av[SMALL_GG];
+#pragma unroll
+        for (int i = 0; i < SMALL_GG; ++i) av[i] = AcmI[(long)(4 * q + lr) * m_pad + 16 * (w * GBW + g4 + i) + lc];
+        const double hv = sm.H[lc][4 * q + lr];
+#pragma unroll
+        for (int i = 0; i < SMALL_GG; ++i) f[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], hv, f[i], 0, 0, 0);
+      }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        e = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.T[w][lc][4 * q + lr], sm.S[4 * q + lr][lc], e, 0, 0, 0);
+      for (int q = 0; q < 4; ++q) {
+        const double sv = sm.S[4 * q + lr][lc];
+#pragma unroll
+        for (int i = 0; i < SMALL_GG; ++i)
+          e[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.T[w][i][lc][4 * q + lr], sv, e[i], 0, 0, 0);
+      }
       __builtin_amdgcn_wave_barrier();
       if (upd) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) wr[gb][r] = mu_rule(wr[gb][r], f[r], e[r]);
+        for (int i = 0; i < SMALL_GG; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) wr[g4 + i][r] = mu_rule(wr[g4 + i][r], f[i][r], e[i][r]);
       }
-      __builtin_amdgcn_sched_barrier(0);   // one gene block's loads in flight at a time
+      __builtin_amdgcn_sched_barrier(0);   // one group's loads in flight at a time
     }
     // ---- stop bookkeeping (one thread), then every thread sees the new run flags ----
     if (tid == 0) {

@@ -85,6 +85,21 @@ def test_check_matrices():
     assert libnmf.checkMatrices(a, w, h) == 1
 
 
+@pytest.mark.parametrize("k", [1, 17])
+def test_nmf_mu_rank_limit(capfd, k):
+    # libnmf_compat.h: k outside 2..min(16, m, n) is refused before any device work, factors untouched
+    from nmfconsensus_amd import libnmf
+    rng = np.random.default_rng(0)
+    a = rng.random((40, 20)) + 0.1
+    w0, h0 = rng.random((40, k)), rng.random((k, 20))
+    w_in, h_in = w0.copy(), h0.copy()
+    out = libnmf.nmf_mu(a, w0, h0, 100)
+    assert out["ret"] == -1 and out["maxiter"] == 100
+    assert np.array_equal(out["w0"], w_in) and np.array_equal(out["h0"], h_in)
+    err = capfd.readouterr().err
+    assert f"Error in nmf_mu: nmfc_engine_run: k={k} unsupported (need 2 <= k <= min(16, m, n))" in err
+
+
 def test_generate_matrix_follows_libc_stream(golden):
     # generateMatrix(ran) draws W then H from libc rand() (generatematrix.c:131-137): after the first
     # randnumber call trips srand(time) (randnumber.c:29-33), srand(123) reproduces the golden init.

@@ -327,3 +327,23 @@ def test_narrow_end_kernels_bit_identical(oracle, golden, m, n, ks, R):
     W0, H0 = oracle.init_restart(3, m, n, k)
     Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, 14, 0)
     assert relfro(runs[0].W[0], Wo) < TOL and relfro(runs[0].H[0], Ho) < TOL
+
+
+def test_small_path_agrees_with_batched_engine(golden):
+    """The small-shape persistent kernel (m_pad <= 1024, n <= 64) and the batched three-kernel engine sum in
+    different fixed orders: on the C1 sweep they agree to rounding (W/H) and exactly (exits, labels)."""
+    import os
+    from nmfconsensus_amd.nmf import Engine
+    runs = []
+    try:
+        for flag in ("1", "0"):
+            os.environ["NMFC_SMALL"] = flag
+            with Engine(golden["A_gct"]) as eng:
+                runs.append(eng.run([2, 3, 4, 5], 6, maxiter=10000, seed=123, stop_rule=1, want_factors=True))
+    finally:
+        os.environ.pop("NMFC_SMALL", None)
+    a, b = runs
+    assert np.array_equal(a.iters, b.iters) and np.array_equal(a.labels, b.labels)
+    assert np.array_equal(a.counts, b.counts)
+    for j in range(24):
+        assert relfro(a.W[j], b.W[j]) < 1e-11 and relfro(a.H[j], b.H[j]) < 1e-11
