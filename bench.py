@@ -140,6 +140,8 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=100, help="iterations per k in the CPU sample (~20 s wall on 16 cores)")
     ap.add_argument("--cpu-cores", type=int, default=None)
     ap.add_argument("--no-timing", action="store_true", help="disable per-launch HIP event timing")
+    ap.add_argument("--timing-stride", type=int, default=4,
+                    help="event-time the launches of every S-th MU iteration (a uniform sample; S=1 times all)")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="strong (default): the fixed R restarts per k are split over the N GPUs (the north-star "
                          "job); weak: every GPU runs the full per-GPU workload (R restarts per k each, consensus "
@@ -207,7 +209,7 @@ def main():
     eng.set_timing(False)
     for _ in range(args.warmup):
         step()
-    eng.set_timing(timing)
+    eng.set_timing(timing, args.timing_stride)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -280,8 +282,11 @@ def main():
                 "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
                 "algo_bytes_per_launch": kernels[dom]["algo_bytes_per_launch"], "kernels": kernels,
                 "note": ("achieved = algorithmic flop per launch (SURVEY 8(d): 2mnk + 2mk^2 per live restart) / "
-                         "the kernel's mean HIP-event duration over every launch of the timed sweeps; kernels[*] "
-                         "with bound 'hbm': algorithmic bytes per launch / mean duration vs 8 TB/s")}
+                         "the kernel's mean HIP-event duration over the timed launches of the timed sweeps (every "
+                         f"{args.timing_stride}th MU iteration's launches, a uniform sample, plus every labels/counts "
+                         "launch; 'launches' counts the timed ones); kernels[*] with bound 'hbm': algorithmic bytes "
+                         "per launch / mean duration vs 8 TB/s"),
+                "timing_stride": args.timing_stride}
         tp = pmc_profile_for(args.config, dom)
         if tp:
             roof["traffic"], roof["traffic_unit"] = tp

@@ -171,7 +171,10 @@ const char* nmfc_version(void);
  * 6 = connectivity counts, 7 = small-shape persistent MU kernel (m_pad <= 1024, n <= 64: the whole
  * loop in one launch).  Returns the number of launches of that kernel. */
 long long nmfc_engine_kernel_time(nmfc_engine* e, int kernel_id, double* ms_out);
-/* Enables per-launch event timing (adds small overhead; used by bench.py's roofline leg). */
+/* enable = 0: no event timing; enable = S >= 1: HIP events around every launch of every S-th MU
+ * iteration (and every other launch), so kernel_time returns the TIMED launches and their summed ms
+ * (a uniform sample of the run; used by bench.py's roofline leg).  Flop/byte figures are per launch
+ * over all launches. */
 void nmfc_engine_set_timing(nmfc_engine* e, int enable);
 /* Algorithmic flop per launch of the dominant kernel in the last run, for the roofline report. */
 double nmfc_engine_kernel_flops(nmfc_engine* e, int kernel_id);

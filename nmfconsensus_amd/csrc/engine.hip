@@ -172,12 +172,56 @@ Packing pack(const std::vector<RestartInfo>& in) {
   return pk;
 }
 
-// every restart of the packing lies in columns 0..15 of panel 0 (the narrow end-of-sweep kernels apply)
-bool narrow_packing(const Packing& pk) {
-  if (pk.ri.empty()) return false;
+// Narrow (end-of-sweep) form: every restart of the packing inside one 16-column block, all of them in the
+// first nb <= maxb blocks -> nb (the narrow kernels run only those blocks); otherwise 0.
+int narrow_blocks(const Packing& pk, int maxb) {
+  if (pk.ri.empty()) return 0;
+  int nb = 0;
+  for (const RestartInfo& r : pk.ri) {
+    if (r.col0 / 16 != (r.col0 + r.k - 1) / 16) return 0;
+    nb = std::max(nb, (r.col0 + r.k + 15) / 16);
+  }
+  return nb <= maxb ? nb : 0;
+}
+
+// Block packing for the tail: restarts first-fit decreasing into 16-column blocks (a restart never straddles
+// a block), blocks in order from column 0, so a few live restarts occupy only a few narrow blocks.
+Packing pack_blocks(const std::vector<RestartInfo>& in, int& nblocks) {
+  std::vector<RestartInfo> srt(in);
+  std::stable_sort(srt.begin(), srt.end(), [](const RestartInfo& a, const RestartInfo& b) {
+    return a.k != b.k ? a.k > b.k : a.rid < b.rid;
+  });
+  std::vector<int> fill;
+  std::vector<std::vector<RestartInfo>> members;
+  for (RestartInfo r : srt) {
+    size_t b = 0;
+    while (b < fill.size() && fill[b] + r.k > 16) ++b;
+    if (b == fill.size()) {
+      fill.push_back(0);
+      members.emplace_back();
+    }
+    r.col0 = (int)b * 16 + fill[b];
+    fill[b] += r.k;
+    members[b].push_back(r);
+  }
+  nblocks = (int)members.size();
+  Packing pk;
+  pk.npanels = std::max(1, (nblocks + 3) / 4);
+  for (int p = 0; p < pk.npanels; ++p) {   // a panel = 4 consecutive blocks
+    pk.prb.push_back((int)pk.ri.size());
+    for (int b = 4 * p; b < std::min(nblocks, 4 * p + 4); ++b)
+      for (const RestartInfo& r : members[b]) pk.ri.push_back(r);
+    pk.pre.push_back((int)pk.ri.size());
+  }
+  while (pk.npanels % WTA_NPT) {
+    pk.prb.push_back((int)in.size());
+    pk.pre.push_back((int)in.size());
+    ++pk.npanels;
+  }
+  pk.ci.assign((size_t)pk.npanels * PANEL, ColInfo{0, 0, 0, 0});
   for (const RestartInfo& r : pk.ri)
-    if (r.col0 + r.k > 16) return false;
-  return true;
+    for (int a = 0; a < r.k; ++a) pk.ci[r.col0 + a] = ColInfo{r.sq_off, r.col0 % PANEL, r.k, r.rid};
+  return pk;
 }
 
 // Small-shape path (k_small_mu): restarts packed first-fit decreasing into 16-column blocks (a restart never
@@ -239,6 +283,7 @@ struct nmfc_engine {
   int force_wta = -1, force_ahtw = -1;   // tile-shape overrides (env NMFC_WTA_TILE / NMFC_AHTW_TILE)
   int repack_div = 5;                     // repack after nact / repack_div stops (env NMFC_REPACK_DIV)
   bool narrow_ok = true;                  // narrow end-of-sweep kernels allowed (env NMFC_NARROW=0 disables)
+  int narrow_maxb = 3;                    // narrow form up to this many 16-column blocks (env NMFC_NARROW_MAXB)
   bool small_ok = true;                   // small-shape persistent kernel allowed (env NMFC_SMALL=0 disables)
   DevBuf Acm, Arm;
   // per-run buffers (grow-only)
@@ -250,6 +295,7 @@ struct nmfc_engine {
   int* h_stopped = nullptr;   // pinned, 2 slots
   // timing
   bool timing = false;
+  int timing_stride = 1;            // time the launches of every timing_stride-th MU iteration
   std::vector<hipEvent_t> ev_pool;
   struct Pending {
     int kid;
@@ -257,7 +303,8 @@ struct nmfc_engine {
   };
   std::vector<Pending> pending;
   double kms[KID_N] = {0};
-  long long kcount[KID_N] = {0};
+  long long kcount[KID_N] = {0};    // timed launches (event pairs drained)
+  long long klaunch[KID_N] = {0};   // every launch
   double kflops[KID_N] = {0};
   double kbytes[KID_N] = {0};       // bytes the kernel's design moves per launch (operands + partials)
   double kbytes_algo[KID_N] = {0};  // algorithmic bytes per launch (each operand once)
@@ -375,21 +422,23 @@ struct TimedLaunch {
   nmfc_engine* e;
   int kid;
   hipEvent_t a = nullptr;
-  TimedLaunch(nmfc_engine* e_, int kid_) : e(e_), kid(kid_) {
-    if (e->timing) {
+  // sample = false: counted, not timed (the MU loop times every timing_stride-th iteration)
+  TimedLaunch(nmfc_engine* e_, int kid_, bool sample = true) : e(e_), kid(kid_) {
+    e->klaunch[kid] += 1;
+    if (e->timing && sample) {
       a = take_event(e);
       if (a) (void)hipEventRecord(a, e->st);
     }
   }
   ~TimedLaunch() {
-    if (e->timing && a) {
+    if (a) {
       hipEvent_t b = take_event(e);
       if (b) {
         (void)hipEventRecord(b, e->st);
         e->pending.push_back({kid, a, b});
+      } else {
+        e->ev_pool.push_back(a);
       }
-    } else if (!e->timing) {
-      e->kcount[kid] += 1;
     }
   }
 };
@@ -443,6 +492,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   }
   if (const char* s = getenv("NMFC_REPACK_DIV")) e->repack_div = std::max(1, atoi(s));
   if (const char* s = getenv("NMFC_NARROW")) e->narrow_ok = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_NARROW_MAXB")) e->narrow_maxb = std::min(8, std::max(1, atoi(s)));
   if (const char* s = getenv("NMFC_SMALL")) e->small_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
     const std::string v(s);
@@ -457,7 +507,12 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   e->n_cols_pad = round_up(n, 128);    // sample tiles of W^T A
   e->ngt = (int)(e->m_pad / GT);
   // fixed gene chunks of W^T A: a function of m only, so every entry's summation order is batch-independent
-  e->kchunk = (int)std::min<long>(2048, e->m_pad);
+  int kchunk = 2048;   // canonical split-K chunk; NMFC_KCHUNK (512 | 1024 | 2048 | 4096) is a probe knob
+  if (const char* v = getenv("NMFC_KCHUNK")) {
+    const int x = atoi(v);
+    if (x == 512 || x == 1024 || x == 2048 || x == 4096) kchunk = x;
+  }
+  e->kchunk = (int)std::min<long>(kchunk, e->m_pad);
   e->nsplit = (int)((e->m_pad + e->kchunk - 1) / e->kchunk);
   if (e->Acm.ensure(sizeof(double) * e->n_cols_pad * e->m_pad) || e->Arm.ensure(sizeof(double) * e->m_pad * e->n_pad)) {
     nmfc_engine_destroy(e);
@@ -504,7 +559,9 @@ void nmfc_engine_destroy(nmfc_engine* e) {
 }
 
 void nmfc_engine_set_timing(nmfc_engine* e, int enable) {
-  if (e) e->timing = enable != 0;
+  if (!e) return;
+  e->timing = enable > 0;
+  e->timing_stride = std::max(1, enable);
 }
 
 long long nmfc_engine_kernel_time(nmfc_engine* e, int kid, double* ms_out) {
@@ -558,6 +615,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   for (int q = 0; q < KID_N; ++q) {
     e->kms[q] = 0;
     e->kcount[q] = 0;
+    e->klaunch[q] = 0;
     e->kflops[q] = 0;
     e->kbytes[q] = 0;
     e->kbytes_algo[q] = 0;
@@ -776,8 +834,9 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       const TileChoice tc = choose_tiles(e, live_panels(pk), ntj);
       bool wta_big = tc.wta == 0, wta_mid = tc.wta == 3, wta_tiny = tc.wta == 2;
       bool ahtw_small = tc.ahtw_small;
-      // narrow (end-of-sweep) form: every restart of the packing inside columns 0..15 of panel 0
-      const bool narrow = e->narrow_ok && narrow_packing(pk);
+      // narrow (end-of-sweep) form: the restarts block-packed into the first nblk 16-column blocks
+      const int nblk = e->narrow_ok ? narrow_blocks(pk, e->narrow_maxb) : 0;
+      const bool narrow = nblk > 0;
       const int ngt_ahtw = e->ngt * (ahtw_small ? 2 : 1);
       const int grid_ahtw = pk.npanels * ngt_ahtw;
       for (int c = 1; c <= chunk; ++c) {
@@ -786,11 +845,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           // W^T A on the GTile core: 4-panel x 128-sample tiles (8 waves) while the grid fills the chip
           // at least twice, else 1-panel x 64-sample tiles (4 waves).  Both accumulate every entry in
           // the same canonical K order, so the switch never changes a bit.
-          TimedLaunch tl(e, KID_WTA);
+          TimedLaunch tl(e, KID_WTA, iter % e->timing_stride == 0);
           if (narrow) {
             const int ntq = (int)(e->n_cols_pad / 16);
-            hipLaunchKernelGGL((k_wta_narrow<16, 4>), dim3(e->nsplit * ntq), dim3(64), 0, st, e->W[cur].as<double>(),
-                               e->Acm.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, e->colinfo.as<ColInfo>(),
+            hipLaunchKernelGGL((k_wta_narrow<16, 4>), dim3(e->nsplit * nblk * ntq), dim3(64), 0, st,
+                               e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
+                               e->colinfo.as<ColInfo>(),
                                e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
@@ -815,8 +875,11 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
                                e->SWpart.as<double>(), sw_total);
-          } else {   // few live panels: 1-panel x 32-sample tiles, two 16x16 blocks per wave (short chains)
-            hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1>), dim3(e->nsplit * pk.npanels * 4 * ntj), dim3(256), 0, st,
+          } else {   // few live panels: 1-panel x 32-sample tiles, two 16x16 blocks per wave (short chains);
+                     // at most one live workgroup per CU: an 8-stage ring (more DMA in flight per CU, 96 KiB)
+            auto kw = (long)e->nsplit * live_panels(pk) * 4 * ntj <= e->ncu ? k_wta2<1, 32, 4, 1, 1, 8>
+                                                                             : k_wta2<1, 32, 4, 1, 1>;
+            hipLaunchKernelGGL(kw, dim3(e->nsplit * pk.npanels * 4 * ntj), dim3(256), 0, st,
                                e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, pk.npanels, 4 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
@@ -824,7 +887,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           }
         }
         {
-          TimedLaunch tl(e, KID_HUPD);
+          TimedLaunch tl(e, KID_HUPD, iter % e->timing_stride == 0);
           hipLaunchKernelGGL(k_hupdate, dim3(nact), dim3(NTH), 0, st, iter, opts.maxiter, opts.stop_rule,
                              e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, e->nsplit,
                              e->SWpart.as<double>(), sw_total, e->H[cur].as<double>(), e->SH.as<double>(),
@@ -838,11 +901,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           HCHECK(hipMemcpyAsync(e->Wsnap.p, e->W[cur].p, sizeof(double) * (size_t)pk.npanels * PANEL * e->m_pad,
                                 hipMemcpyDeviceToDevice, st));
         {
-          TimedLaunch tl(e, KID_AHTW);
-          if (narrow) {   // 16 rows x 32 genes, 2 waves
-            hipLaunchKernelGGL((k_ahtw4<0, GT / 4, GT_NBUF, 1, 16, 2>), dim3(4 * e->ngt), dim3(128), 0, st, iter,
-                               e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
-                               e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), 1, 4 * e->ngt);
+          TimedLaunch tl(e, KID_AHTW, iter % e->timing_stride == 0);
+          if (narrow) {   // per live 16-column block: 16 rows x 32 genes, 2 waves
+            hipLaunchKernelGGL((k_ahtw4<0, GT / 4, GT_NBUF, 1, 16, 2>), dim3(4 * e->ngt * nblk), dim3(128), 0, st,
+                               iter, e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad,
+                               e->W[cur].as<double>(), e->SHP.as<double>(), e->colinfo.as<ColInfo>(),
+                               e->colact.as<int>(), nblk, 4 * e->ngt);
           } else {
             auto ka = ahtw_small ? k_ahtw4<0, GT / 2> : k_ahtw4<0, GT>;
             hipLaunchKernelGGL(ka, dim3(grid_ahtw), dim3(256), 0, st, iter,
@@ -887,6 +951,14 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       for (const RestartInfo& r : pk.ri) (si[r.rid] ? gone : live).push_back(r);
       if (archive(gone)) return -1;
       Packing np = pack(live);
+      if (e->narrow_ok) {   // few live columns: block packing, so the narrow kernels run only the live blocks
+        int cols = 0, nb = 0;
+        for (const RestartInfo& r : live) cols += r.k;
+        if (cols <= 16 * e->narrow_maxb) {
+          Packing bp = pack_blocks(live, nb);
+          if (nb <= e->narrow_maxb && (long)bp.npanels * PANEL <= cap_cols) np = std::move(bp);
+        }
+      }
       if ((long)np.npanels * PANEL > cap_cols) {
         // first-fit decreasing is not monotone under removal: a (rare) larger packing would overrun
         // the buffers sized from the initial one, so keep the current placement until the next poll
@@ -1012,27 +1084,27 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     if (out && out->stopped_early) out->stopped_early[rslot[rid]] = (sr[rid] == 1 || sr[rid] == 3);
   }
   const double a_bytes = 8.0 * m * n;   // A, read once per launch by each contraction
-  if (const long long c = e->kcount[KID_WTA]) {
+  if (const long long c = e->klaunch[KID_WTA]) {
     e->kflops[KID_WTA] = fl_wta / c;
     e->kbytes_algo[KID_WTA] = a_bytes + ba_wta / c;
     e->kbytes[KID_WTA] = a_bytes + b_wta / c;
   }
-  if (const long long c = e->kcount[KID_AHTW]) {
+  if (const long long c = e->klaunch[KID_AHTW]) {
     e->kflops[KID_AHTW] = fl_ahtw / c;
     e->kbytes_algo[KID_AHTW] = a_bytes + ba_ahtw / c;
     e->kbytes[KID_AHTW] = a_bytes + b_ahtw / c;
   }
-  if (const long long c = e->kcount[KID_SMALL]) {   // the whole MU iteration in one persistent launch
+  if (const long long c = e->klaunch[KID_SMALL]) {   // the whole MU iteration in one persistent launch
     e->kflops[KID_SMALL] = (fl_wta + fl_ahtw) / c;
     e->kbytes_algo[KID_SMALL] = (ba_wta + ba_ahtw + ba_hupd) / c;
     e->kbytes[KID_SMALL] = e->kbytes_algo[KID_SMALL];
   }
-  if (const long long c = e->kcount[KID_HUPD]) {
+  if (const long long c = e->klaunch[KID_HUPD]) {
     e->kbytes_algo[KID_HUPD] = ba_hupd / c;
     e->kbytes[KID_HUPD] = b_hupd / c;
   }
-  if (e->kcount[KID_LABELS]) e->kbytes[KID_LABELS] = e->kbytes_algo[KID_LABELS] = b_lab;   // one launch
-  if (e->kcount[KID_COUNTS]) {   // labels of each k group read once, n x n int32 counts written per k
+  if (e->klaunch[KID_LABELS]) e->kbytes[KID_LABELS] = e->kbytes_algo[KID_LABELS] = b_lab;   // one launch
+  if (e->klaunch[KID_COUNTS]) {   // labels of each k group read once, n x n int32 counts written per k
     e->kbytes_algo[KID_COUNTS] = 4.0 * nj * n + 4.0 * nk * n * n;
     e->kbytes[KID_COUNTS] = e->kbytes_algo[KID_COUNTS];
   }

@@ -427,22 +427,23 @@ static __global__ __launch_bounds__(WR * WC * 64) void k_wta2(const double* __re
 }
 
 // ---------------------------------------------------------------------------------------------
-// K1 narrow form (the tail: every live restart inside columns 0..15 of panel 0): G rows 0..15 = W^T A
-// over the same fixed gene chunks, one wave per (chunk, RQ-sample tile), RP = 16 rows -- a quarter of
-// the W bytes per sample tile of the 64-row tiles, so many more, lighter workgroups.  The tile's
-// accumulation is the canonical GTile K order, so the rows are bit-identical to every other shape.
-// Tile t == 0 of each chunk also forms the 16 x 16 Gram block of those columns (nmf_mu.c:176).
+// K1 narrow form (the tail: the live restarts block-packed into the first nblk 16-column blocks, none
+// straddling a block): G rows 16 b .. 16 b + 15 = W^T A over the same fixed gene chunks, one wave per
+// (chunk, block, RQ-sample tile), RP = 16 rows -- only the live blocks' MFMA work, and many more, lighter
+// workgroups than the 64-row tiles.  The accumulation is the canonical GTile K order, so the rows are
+// bit-identical to every other shape.  Tile t == 0 of each (chunk, block) also forms the block's 16 x 16
+// Gram block (nmf_mu.c:176); no restart crosses a block, so that is every Gram entry of its restarts.
 // ---------------------------------------------------------------------------------------------
 template <int RQ, int NBUF>
 static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restrict__ W, const double* __restrict__ Acm,
-                                                          long m_pad, int ntq, int nsplit, int kchunk,
+                                                          long m_pad, int ntq, int nsplit, int kchunk, int nblk,
                                                           const ColInfo* __restrict__ ci, double* __restrict__ Gpart,
                                                           long g_ld, long g_split, double* __restrict__ SWpart,
                                                           long sw_total) {
   using T = GTile<16, RQ, 1, 1, NBUF>;
   __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES];
-  const int item = xcd_item(blockIdx.x, nsplit * ntq);
-  const int t = item % ntq, s = item / ntq;
+  const int item = xcd_item(blockIdx.x, nsplit * nblk * ntq);
+  const int t = item % ntq, bk = (item / ntq) % nblk, s = item / (ntq * nblk);
   const int kbeg = s * kchunk;
   const int kend = (int)min((long)kbeg + kchunk, m_pad);
   const int l = threadIdx.x, fr = l & 15, g = l >> 4;
@@ -450,7 +451,7 @@ static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restri
   T tl;
   tl.zero();
   d4 gacc = (d4){0.0, 0.0, 0.0, 0.0};
-  tl.run(W, m_pad, Acm + (long)t * RQ * m_pad, m_pad, kbeg, kend, smem, [&](const char* stg) {
+  tl.run(W + (long)bk * 16 * m_pad, m_pad, Acm + (long)t * RQ * m_pad, m_pad, kbeg, kend, smem, [&](const char* stg) {
     if (!gram) return;
     const char* pa = stg + fr * 128;
 #pragma unroll
@@ -460,19 +461,20 @@ static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restri
       gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, a.y, gacc, 0, 0, 0);
     }
   });
-  double* out = Gpart + (long)s * g_split + (long)t * RQ;
+  double* out = Gpart + (long)s * g_split + (long)bk * 16 * g_ld + (long)t * RQ;
 #pragma unroll
   for (int nb = 0; nb < T::NB; ++nb)
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) out[(long)T::row_of(0, reg) * g_ld + T::col_of(nb)] = tl.acc[0][nb][reg];
   if (gram) {
     double* so = SWpart + (long)s * sw_total;
+    const ColInfo* cb = ci + (long)bk * 16;
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int lr = g + 4 * reg, lcn = fr;
-      const ColInfo cr = ci[lr];
-      if (cr.k == 0 || cr.lc0 != ci[lcn].lc0 || ci[lcn].k == 0) continue;   // not the same restart
-      const int a = lr - cr.lc0, b = lcn - cr.lc0;
+      const ColInfo cr = cb[lr];
+      if (cr.k == 0 || cr.lc0 != cb[lcn].lc0 || cb[lcn].k == 0) continue;   // not the same restart
+      const int a = lr - (cr.lc0 & 15), b = lcn - (cr.lc0 & 15);
       so[cr.sq_off + a * cr.k + b] = gacc[reg];
       so[cr.sq_off + b * cr.k + a] = gacc[reg];
     }
@@ -771,7 +773,7 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
   constexpr int AHTW4_SH = TileW4::LDS_BYTES;
   constexpr int AHTW4_LDS = AHTW4_SH + NPT * PR * KMAX * 8;
   static_assert(AHTW4_LDS <= 163840, "LDS of one CU");
-  static_assert(PR == PANEL || NPT == 1, "narrow tiles cover one panel");
+  static_assert(PR == PANEL || (PR == 16 && NPT == 1), "narrow tiles: one 16-column block");
   constexpr int NTH = 64 * NPT * WC;
   __shared__ __attribute__((aligned(1024))) char smem[AHTW4_LDS];
   double* SHl = reinterpret_cast<double*>(smem + AHTW4_SH);
@@ -784,16 +786,17 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
   uint64_t actmask = 0;
   TileW4 tl;
   tl.zero();
-  const double* wsrc = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / WC) * wc + (lane & 15);
+  // PR = 16: the "panel" index p is a 16-column block (column 16 p of the stacked W / H)
+  const double* wsrc = W + (long)p * PR * m_pad + (long)gt * GTG + (GTG / WC) * wc + (lane & 15);
   double w0[TileW4::MB][TileW4::NB][4];
   const bool live = tl.template run<TileW4::MB * TileW4::NB * 4>(
-      H + (long)p0 * PANEL * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
+      H + (long)p0 * PR * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
       [&] {   // setup loads, independent of each other, overlapping the first stages' DMA
-        cc = ci[(long)p * PANEL + lane];
+        cc = lane < PR ? ci[(long)p * PR + lane] : ColInfo{0, 0, 0, 0};
         int ca[NPT];
 #pragma unroll
-        for (int q = 0; q < NPT; ++q) ca[q] = colact[(long)(p0 + q) * PANEL + lane];
-        const d2* src = reinterpret_cast<const d2*>(SHP + (long)p0 * PANEL * KMAX);
+        for (int q = 0; q < NPT; ++q) ca[q] = lane < PR ? colact[(long)(p0 + q) * PR + lane] : -1;
+        const d2* src = reinterpret_cast<const d2*>(SHP + (long)p0 * PR * KMAX);
         constexpr int NSH = NPT * PR * KMAX / 2 / NTH;
         static_assert(NSH * 2 * NTH == NPT * PR * KMAX, "h h^T rows split evenly over the threads");
         d2 shv[NSH];
@@ -825,12 +828,12 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
       });
   if (!live) return;
   if (actmask == 0) return;   // this wave's panel is idle (its partner panel is not)
-  double* wdst = W + (long)p * PANEL * m_pad + (long)gt * GTG + (GTG / WC) * wc + (lane & 15);
+  double* wdst = W + (long)p * PR * m_pad + (long)gt * GTG + (GTG / WC) * wc + (lane & 15);
   const double* SHw = SHl + (long)wr * PR * KMAX;
 #pragma unroll
   for (int mb = 0; mb < TileW4::MB; ++mb) {
     const int ra = 16 * mb + (lane & 15);
-    const int alc = __shfl(cc.lc0, ra);
+    const int alc = __shfl(cc.lc0, ra) & (PR - 1);   // tile-local (a restart never straddles a tile)
     const int ak = (VARIANT == 2 || VARIANT == 4 || !((actmask >> ra) & 1)) ? 0 : __shfl(cc.k, ra);
     int lo = ak ? alc : PANEL, hi = ak ? alc + ak : 0;
 #pragma unroll

@@ -120,8 +120,9 @@ class Engine:
     def __exit__(self, *exc):
         self.close()
 
-    def set_timing(self, on: bool):
-        self.L.nmfc_engine_set_timing(self.h, 1 if on else 0)
+    def set_timing(self, on: bool, stride: int = 1):
+        """Event-time the launches of every `stride`-th MU iteration (nmfc_engine_set_timing)."""
+        self.L.nmfc_engine_set_timing(self.h, max(1, int(stride)) if on else 0)
 
     def kernel_time(self, kid: int):
         ms = ctypes.c_double(0.0)

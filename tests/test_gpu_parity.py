@@ -306,27 +306,52 @@ def test_c2_sweep_vs_reference(golden_c2, rule, key):
 
 
 @pytest.mark.parametrize("m,n,ks,R", [(1000, 40, [2, 3, 5], 1), (3001, 150, [7, 9], 1), (97, 33, [5], 2),
-                                      (2500, 300, [16], 1)])
+                                      (2500, 300, [16], 1), (2000, 120, [16, 16, 8, 8], 1)])
 def test_narrow_end_kernels_bit_identical(oracle, golden, m, n, ks, R):
-    """The narrow end-of-sweep kernels (every restart inside columns 0..15 of panel 0) accumulate in the same
-    canonical K order as the 64-row tiles: W/H bit-identical with them disabled (NMFC_NARROW=0)."""
+    """The narrow end-of-sweep kernels (the restarts inside the first 1..3 16-column blocks, none straddling a
+    block) accumulate in the same canonical K order as the 64-row tiles: W/H bit-identical with them disabled
+    (NMFC_NARROW=0).  The last case spans three blocks."""
     import os
     from nmfconsensus_amd.nmf import Engine
     A = golden["A_gct"] if (m, n) == (1000, 40) else np.asfortranarray(np.random.default_rng(m + n).random((m, n)))
     runs = []
     try:
+        os.environ["NMFC_SMALL"] = "0"   # keep the 1000 x 40 case on the batched kernels
         for flag in ("1", "0"):
             os.environ["NMFC_NARROW"] = flag
             with Engine(A) as eng:
                 runs.append(eng.run(ks, R, maxiter=14, seed=3, stop_rule=0, want_factors=True))
     finally:
         os.environ.pop("NMFC_NARROW", None)
+        os.environ.pop("NMFC_SMALL", None)
     for j in range(len(ks) * R):
         assert np.array_equal(runs[0].W[j], runs[1].W[j]) and np.array_equal(runs[0].H[j], runs[1].H[j]), j
     k = ks[0]
     W0, H0 = oracle.init_restart(3, m, n, k)
     Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, 14, 0)
     assert relfro(runs[0].W[0], Wo) < TOL and relfro(runs[0].H[0], Ho) < TOL
+
+
+def test_block_packed_tail_bit_identical():
+    """A REF_COMPAT sweep whose tail is repacked into 16-column blocks and run by the narrow kernels gives the
+    same exits, labels, counts and bit-identical W/H as the same sweep on the 64-row panel kernels."""
+    import os
+    from nmfconsensus_amd.nmf import Engine
+    A = np.asfortranarray(np.random.default_rng(7).random((3001, 150)))
+    runs = []
+    try:
+        for flag in ("1", "0"):
+            os.environ["NMFC_NARROW"] = flag
+            with Engine(A) as eng:
+                runs.append(eng.run([2, 3, 4, 5, 6], 4, maxiter=3000, seed=11, stop_rule=1, want_factors=True))
+    finally:
+        os.environ.pop("NMFC_NARROW", None)
+    a, b = runs
+    assert np.array_equal(a.iters, b.iters) and np.array_equal(a.labels, b.labels)
+    assert np.array_equal(a.counts, b.counts)
+    assert len(set(a.iters.tolist())) > 3   # restarts stop at different iterations: the tail is repacked
+    for j in range(20):
+        assert np.array_equal(a.W[j], b.W[j]) and np.array_equal(a.H[j], b.H[j]), j
 
 
 def test_small_path_agrees_with_batched_engine(golden):

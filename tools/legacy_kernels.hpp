@@ -595,3 +595,199 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw2(int iter, const double*
 }
 
 }  // namespace nmfc
+
+// ---------------------------------------------------------------------------------------------
+// Round-2 experiment, not kept: a persistent A h^T kernel that pipelines ACROSS tiles (the next tile's
+// setup loads, h h^T rows and first ring stages are issued before the current tile's epilogue; W0 via
+// untracked loads so the compiler's vmcnt insertion does not drain that DMA).  Bit-identical, but on C3
+// it measured 49.7 TF vs 50.4 TF for k_ahtw4 (and slower on the R = 25 shard): the static round-robin
+// tile walk loses more to imbalance than the overlap wins (gpurun_out r02n).
+// ---------------------------------------------------------------------------------------------
+namespace nmfc {
+// A global load the compiler's wait-count insertion does not see (the caller waits with wait_vmcnt).
+__device__ __forceinline__ double load_untracked(const double* p) {
+  double v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+// p[0] and p[16] (one address register pair for both)
+__device__ __forceinline__ void load_untracked2(const double* p, double& a, double& b) {
+  asm volatile("global_load_dwordx2 %0, %2, off\n\tglobal_load_dwordx2 %1, %2, off offset:128"
+               : "=&v"(a), "=&v"(b)
+               : "v"(p)
+               : "memory");
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3 persistent form "ahtw_p" (the full-load shape of k_ahtw4: 1 panel x GTG genes, 4 waves, 2 workgroups
+// per CU): each workgroup walks the items v = blockIdx.x, + gridDim.x, ... (same item map) and pipelines
+// ACROSS tiles -- right after a tile's last MFMA stage it issues the next live tile's setup loads and its
+// first D ring stages, then runs the tile's epilogue (E = W0 (h h^T) on MFMA, W rule, W stores) while that
+// DMA is in flight.  The per-tile ring fill latency and the epilogue no longer leave the matrix pipe idle
+// between tiles.  The arithmetic of every output is exactly k_ahtw4's (same K order), so it is
+// bit-identical to every other A h^T shape.  Needs n_pad / BK2 >= GT_NBUF - 1 (n_pad >= 32).
+// ---------------------------------------------------------------------------------------------
+template <int GTG = GT>
+static __global__ __launch_bounds__(256, 2) void k_ahtw_p(int iter, const double* __restrict__ H, long n_pad,
+                                                          const double* __restrict__ Arm, long m_pad,
+                                                          double* __restrict__ W, const double* __restrict__ SHP,
+                                                          const ColInfo* __restrict__ ci,
+                                                          const int* __restrict__ colact, int npanels, int ngt) {
+  using TL = GTile<PANEL, GTG, 1, 4, GT_NBUF>;
+  constexpr int D = GT_NBUF - 1;
+  constexpr int XL = TL::MB * TL::NB * 4;   // W0 loads per lane, issued with the tile's last ring stage
+  static_assert(GT_NBUF >= 3 && PANEL * KMAX * 8 == 8192 && TL::STAGE_BYTES >= 8192, "SH rows staged in ring slot D");
+  __shared__ __attribute__((aligned(1024))) char smem[TL::LDS_BYTES + PANEL * KMAX * 8];
+  double* SHl = reinterpret_cast<double*>(smem + TL::LDS_BYTES);
+  const uint32_t base = (uint32_t)(uintptr_t)smem;
+  const int nitems = npanels * ngt;
+  const int nst = (int)(n_pad / BK2);
+  const int tid = threadIdx.x, lane = tid & 63, wc = tid >> 6;
+  TL tl;
+  int v = blockIdx.x, p = 0, gt = 0;
+  int c_lc0 = 0, c_k = 0;   // this lane's column: first panel-local column and k of its restart
+  uint64_t actmask = 0;
+  // claim the next live item from v on: setup loads first, then the tile's h h^T rows (8 KiB, one LDS-DMA
+  // copy into ring slot D, which the K loop refills only at its first step) and the D prologue stages, so
+  // waiting on the setup loads leaves the DMA in flight.  An idle tile (no column updated at this
+  // iteration) is drained and skipped; every wave sees the same ballot.
+  auto claim = [&]() -> bool {
+    for (; v < nitems; v += gridDim.x) {
+      ahtw_map(xcd_item(v, nitems), npanels, ngt, p, gt);
+      const ColInfo* cip = ci + (long)p * PANEL + lane;
+      c_lc0 = cip->lc0;
+      c_k = cip->k;
+      const int ca = colact[(long)p * PANEL + lane];
+      __builtin_amdgcn_sched_barrier(0);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<double*>(SHP + (long)p * PANEL * KMAX), 0, PANEL * KMAX * 8, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        lds_dma16(rs, base + D * TL::STAGE_BYTES + (uint32_t)(wc + 4 * j) * 1024u, (wc + 4 * j) * 1024 + 16 * lane, 0);
+      tl.bind(H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad);
+#pragma unroll
+      for (int q = 0; q < D; ++q) tl.issue(base + q * TL::STAGE_BYTES, q * BK2);
+      __builtin_amdgcn_sched_barrier(0);
+      // (c_k >= 0 keeps the ColInfo loads ahead of the DMA: they complete with ca, before the stages)
+      actmask = __ballot(ca == iter && c_k >= 0);
+      if (actmask != 0) return true;
+      wait_vmcnt<0>();
+    }
+    return false;
+  };
+  if (!claim()) return;
+  bool first = true;
+  for (;;) {
+    const int cp = p, cgt = gt;
+    const int cc_lc0 = c_lc0, cc_k = c_k;
+    const uint64_t cam = actmask;
+    // laundered per tile: otherwise the 32 W0 / W row offsets are hoisted out of the tile loop (registers)
+    long mp = m_pad;
+    asm volatile("" : "+s"(mp));
+    const double* wsrc = W + (long)cp * PANEL * mp + (long)cgt * GTG + (GTG / 4) * wc + (lane & 15);
+    double w0[TL::MB][TL::NB][4];
+    auto load_w0 = [&] {
+#pragma unroll
+      for (int mb = 0; mb < TL::MB; ++mb)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const double* rowp = wsrc + (long)(16 * mb + (lane >> 4) + 4 * reg) * mp;
+          if constexpr (TL::NB == 2)
+            load_untracked2(rowp, w0[mb][0][reg], w0[mb][1][reg]);
+          else
+            w0[mb][0][reg] = load_untracked(rowp);
+        }
+    };
+    tl.zero();
+    bool xl = first ? false : true;   // the previous tile's XL W stores are still in flight
+    if (nst == D) {
+      load_w0();
+      xl = true;
+    }
+    TL::template wait_stages<D - 1, XL>(D - 1, xl);   // stage 0 and (older) the h h^T rows have landed
+    step_barrier();   // ... for every wave; every wave is also past the previous tile's epilogue (SHl free)
+    {
+      const d2* stg = reinterpret_cast<const d2*>(smem + D * TL::STAGE_BYTES);
+      const d2 a0 = stg[tid], a1 = stg[tid + 256];
+      reinterpret_cast<d2*>(SHl)[tid] = a0;
+      reinterpret_cast<d2*>(SHl)[tid + 256] = a1;
+    }
+    step_barrier();   // slot D read by every wave before step 0 refills it; SHl published
+    int b = 0;
+    for (int s = 0; s < nst; ++s) {
+      if (s + D < nst) {
+        const int bd = (b + D >= GT_NBUF) ? b + D - GT_NBUF : b + D;
+        tl.issue(base + bd * TL::STAGE_BYTES, (s + D) * BK2);
+        if (s + D + 1 == nst) {
+          load_w0();
+          xl = true;
+        }
+      }
+      tl.compute(smem + b * TL::STAGE_BYTES);
+      if (s + 1 < nst) {
+        const int left = nst - s - 2;
+        // the stores are older than stage D: from step 1 on, waiting for stage s + 1 covers them
+        if (s + D + 1 < nst && s >= 1) xl = false;
+        TL::template wait_stages<D - 1, XL>(left < D - 1 ? left : D - 1, xl);
+        step_barrier();
+      }
+      b = (b + 1 == GT_NBUF) ? 0 : b + 1;
+    }
+    first = false;
+    step_barrier();   // every wave is done with the ring: the next tile's prologue may refill it
+    v += gridDim.x;
+    const bool more = claim();
+    // W0 came through untracked loads (the compiler would wait for them with vmcnt(0), draining the next
+    // tile's DMA): they are older than the claim's 2 h h^T and D * PPW stage DMA operations
+    if (more)
+      wait_vmcnt<2 + D * TL::PPW>();
+    else
+      wait_vmcnt<0>();
+    // ---- epilogue of (cp, cgt), overlapping the next tile's DMA ----
+    double* wdst = W + (long)cp * PANEL * mp + (long)cgt * GTG + (GTG / 4) * wc + (lane & 15);
+#pragma unroll
+    for (int mb = 0; mb < TL::MB; ++mb) {
+      const int ra = 16 * mb + (lane & 15);
+      const int alc = __shfl(cc_lc0, ra);
+      const int ak = ((cam >> ra) & 1) ? __shfl(cc_k, ra) : 0;
+      int lo = ak ? alc : PANEL, hi = ak ? alc + ak : 0;
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off));
+        hi = max(hi, __shfl_xor(hi, off));
+      }
+      lo = __builtin_amdgcn_readfirstlane(lo);
+      hi = __builtin_amdgcn_readfirstlane(hi);
+      d4 e[TL::NB];
+#pragma unroll
+      for (int nb = 0; nb < TL::NB; ++nb) e[nb] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4 * TL::MB; ++q) {
+        if (4 * q + 3 < lo || 4 * q >= hi) continue;   // wave-uniform
+        const int bb = 4 * q + (lane >> 4) - alc;
+        const double av = (bb >= 0 && bb < ak) ? SHl[ra * KMAX + bb] : 0.0;
+#pragma unroll
+        for (int nb = 0; nb < TL::NB; ++nb)
+          e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, w0[q >> 2][nb][q & 3], e[nb], 0, 0, 0);
+      }
+      // every lane stores (an idle column gets its W0 back, unchanged): a fixed XL stores per tile, so the
+      // next tile's first waits can leave them in flight
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int c = 16 * mb + (lane >> 4) + 4 * reg;
+        const bool act = (cam >> c) & 1;
+#pragma unroll
+        for (int nb = 0; nb < TL::NB; ++nb) {   // mu_rule, branch-free (no execz skips around the stores)
+          const double o = w0[mb][nb][reg], f = tl.acc[mb][nb][reg];
+          const double t = o * (f / (e[nb][reg] + DIV_BY_ZERO_AVOIDANCE));
+          const double nw = (o == 0.0 || f == 0.0 || t < 0.0) ? 0.0 : t;
+          __builtin_nontemporal_store(act ? nw : o, wdst + (long)c * mp + 16 * nb);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // bounded live ranges: no spills
+      }
+    }
+    if (!more) break;
+  }
+}
+
+}  // namespace nmfc
