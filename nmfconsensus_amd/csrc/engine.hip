@@ -375,6 +375,11 @@ hipError_t launch_small_g(nmfc_engine* e, int nblocks, int maxiter, int stop_rul
 
 int launch_small(nmfc_engine* e, int nblocks, int maxiter, int stop_rule) {
   hipError_t err;
+  const int jb = (e->n + 15) / 16;
+  if (e->m_pad % 64 != 0 || e->n_pad != (jb <= 2 ? 32 : 64)) {   // k_small_mu's compile-time strides
+    set_err("k_small_mu: m_pad %ld / n_pad %ld unsupported for n = %d", e->m_pad, e->n_pad, e->n);
+    return -1;
+  }
   switch (e->m_pad / 64) {
     case 2: err = launch_small_g<2>(e, nblocks, maxiter, stop_rule); break;
     case 4: err = launch_small_g<4>(e, nblocks, maxiter, stop_rule); break;

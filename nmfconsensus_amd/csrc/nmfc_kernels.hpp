@@ -885,6 +885,14 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
 // Deterministic: every reduction order is a function of (m, n) only, so a job gives the same bits in
 // any block and any batch.
 // ---------------------------------------------------------------------------------------------
+#ifndef NMFC_SMALL_PF
+#define NMFC_SMALL_PF 8   // k-steps of A rows in flight in the G phase of k_small_mu
+#endif
+constexpr int SMALL_PF = NMFC_SMALL_PF;
+#ifndef NMFC_SMALL_FPF
+#define NMFC_SMALL_FPF 8   // F steps (4 gene blocks each) of A columns in flight
+#endif
+constexpr int SMALL_FPF = NMFC_SMALL_FPF;
 constexpr int SMALL_NW = 4;
 constexpr int SMALL_MAXR = 8;   // restarts per 16-column block (k >= 2)
 constexpr int SMALL_GGMAX = 4;  // gene blocks per F/E group: 4 when GBW % 4 == 0, else 2 (GBW is even)
@@ -915,7 +923,7 @@ struct SmallSmem {
 };
 
 // SKIP != 0 only in tools/smallbench.hip (phase cost breakdown): bit 0 no G/W^T W, 1 no H update,
-// 2 no h h^T / stop rule, 3 no F/E/W update.
+// 2 no h h^T / stop rule, 3 no F/E/W update, 4 no E = W0 (h h^T), 5 W rule replaced by adds.
 template <int GBW, int JB, int SKIP = 0>
 static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     const SmallBlock* __restrict__ blocks, const double* __restrict__ Arm, long ld_rm, const double* __restrict__ Acm,
@@ -953,26 +961,45 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
   for (int iter = 1; iter <= maxiter; ++iter) {
     // the operand base pointers are laundered every iteration: otherwise the compiler hoists the
     // per-k-step addresses of all 4*GBW k-steps out of the iteration loop (hundreds of registers)
-    const double* ArmI = Arm;
-    const double* AcmI = Acm;
-    asm volatile("" : "+s"(ArmI), "+s"(AcmI));
+    // (a laundered zero OFFSET, not a laundered pointer: the pointers keep their global address space, so
+    // the loads stay global_load -- a laundered pointer becomes flat and waits on lgkmcnt too)
+    long zo = 0;
+    asm volatile("" : "+s"(zo));
+    const double* __restrict__ ArmI = Arm + zo;
+    const double* __restrict__ AcmI = Acm + zo;
     // ---- G = W^T A, W^T W over this wave's genes ----
     d4 gacc[JB], sacc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int jb = 0; jb < JB; ++jb) gacc[jb] = (d4){0.0, 0.0, 0.0, 0.0};
+    // software-pipelined: the A rows of k-step t + SMALL_PF are loaded at step t into a register ring
+    // (the loads are L2 hits; issued just before their use they would expose the L2 latency every k-step)
+    {
+      constexpr int NKS = (SKIP & 1) ? 0 : 4 * GBW;
+      double pf[SMALL_PF][JB];
+      constexpr long LDR = (JB <= 2) ? 32 : 64;   // == ld_rm (n_pad = round_up(n, 32), n <= 16 JB; host-checked)
+      const double* __restrict__ arow = ArmI + (long)(16 * w * GBW + lr) * LDR + lc;
 #pragma unroll
-    for (int gb = 0; gb < ((SKIP & 1) ? 0 : GBW); ++gb)
+      for (int t = 0; t < SMALL_PF; ++t)
+        if (t < NKS) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long g = 16 * (w * GBW + gb) + 4 * r + lr;
+          for (int jb = 0; jb < JB; ++jb) pf[t][jb] = arow[(long)(4 * t) * LDR + 16 * jb];
+        }
+#pragma unroll
+      for (int t = 0; t < NKS; ++t) {
+        const int gb = t >> 2, r = t & 3;
         double av[JB];
 #pragma unroll
-        for (int jb = 0; jb < JB; ++jb) av[jb] = ArmI[g * ld_rm + 16 * jb + lc];
+        for (int jb = 0; jb < JB; ++jb) av[jb] = pf[t % SMALL_PF][jb];
+        if (t + SMALL_PF < NKS) {
+#pragma unroll
+          for (int jb = 0; jb < JB; ++jb) pf[t % SMALL_PF][jb] = arow[(long)(4 * (t + SMALL_PF)) * LDR + 16 * jb];
+        }
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb) gacc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(wr[gb][r], av[jb], gacc[jb], 0, 0, 0);
         sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(wr[gb][r], wr[gb][r], sacc, 0, 0, 0);
-        if (r == 3 && (gb & 1)) __builtin_amdgcn_sched_barrier(0);   // loads at most 8 k-steps ahead
+        __builtin_amdgcn_sched_barrier(0);   // keep the issue order: prefetch distance SMALL_PF k-steps
       }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -1077,7 +1104,24 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     const int qmine = sm.colr[lc];
     const bool upd = qmine >= 0 && ((runmask >> qmine) & 1);
     constexpr int SMALL_GG = (GBW % 4 == 0) ? 4 : 2;
-    const int nq = (n + 3) >> 2;
+    constexpr int NQ = NP / 4;                                    // K steps of F (samples, 4 per step)
+    constexpr int NFS = (SKIP & 8) ? 0 : (GBW / SMALL_GG) * NQ;   // (group, K step) pairs of this wave
+    constexpr long MP = 64L * GBW;                                // == m_pad (host-checked)
+    // the A columns of step t + SMALL_PF are loaded at step t into a register ring (rows >= n are in
+    // bounds: Acm holds round_up(n, 128) columns, zero past n)
+    double fpf[SMALL_FPF][SMALL_GG];
+    double hvq[NQ];   // the B operand of every F step (h^T rows), the same for every gene group
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) hvq[q] = sm.H[lc][4 * q + lr];
+    const double* __restrict__ acol = AcmI + (long)lr * MP + 16 * w * GBW + lc;
+    auto f_load = [&](int t, double* dst) {
+      const int g4 = (t / NQ) * SMALL_GG, q = t % NQ;
+#pragma unroll
+      for (int i = 0; i < SMALL_GG; ++i) dst[i] = acol[(long)(4 * q) * MP + 16 * (g4 + i)];
+    };
+#pragma unroll
+    for (int t = 0; t < SMALL_FPF; ++t)
+      if (t < NFS) f_load(t, fpf[t]);
     // GG gene blocks at a time: GG independent MFMA chains for F and for E (a single chain per block would
     // leave the matrix pipe waiting on the dependent-issue latency)
 #pragma unroll
@@ -1088,34 +1132,43 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
         f[i] = (d4){0.0, 0.0, 0.0, 0.0};
         e[i] = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sm.T[w][i][lr + 4 * r][lc] = wr[g4 + i][r];
+        for (int r = 0; r < 4; ++r)
+          if (!(SKIP & 16)) sm.T[w][i][lr + 4 * r][lc] = wr[g4 + i][r];
       }
 #pragma unroll
-      for (int q = 0; q < NP / 4; ++q) {
-        if (q >= nq) break;   // samples >= n: zero rows of h^T (dropping them leaves F bit-identical)
+      for (int q = 0; q < NQ; ++q) {
+        const int t = (g4 / SMALL_GG) * NQ + q;
         double av[SMALL_GG];
 #pragma unroll
-        for (int i = 0; i < SMALL_GG; ++i) av[i] = AcmI[(long)(4 * q + lr) * m_pad + 16 * (w * GBW + g4 + i) + lc];
-        const double hv = sm.H[lc][4 * q + lr];
+        for (int i = 0; i < SMALL_GG; ++i) av[i] = fpf[t % SMALL_FPF][i];
+        if (t + SMALL_FPF < NFS) f_load(t + SMALL_FPF, fpf[t % SMALL_FPF]);
+        // every step, also past n (zero rows of h^T add exact zeros): a data-dependent skip here makes the
+        // compiler shuttle the accumulators between AGPRs and VGPRs around each step
 #pragma unroll
-        for (int i = 0; i < SMALL_GG; ++i) f[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], hv, f[i], 0, 0, 0);
+        for (int i = 0; i < SMALL_GG; ++i) f[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], hvq[q], f[i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);   // keep the prefetch distance
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < ((SKIP & 16) ? 0 : 4); ++q) {
         const double sv = sm.S[4 * q + lr][lc];
 #pragma unroll
         for (int i = 0; i < SMALL_GG; ++i)
           e[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.T[w][i][lc][4 * q + lr], sv, e[i], 0, 0, 0);
       }
       __builtin_amdgcn_wave_barrier();
-      if (upd) {
+      if ((SKIP & 32) && upd) {
+#pragma unroll
+        for (int i = 0; i < SMALL_GG; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) wr[g4 + i][r] += f[i][r] + e[i][r];
+      } else if (upd) {
 #pragma unroll
         for (int i = 0; i < SMALL_GG; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) wr[g4 + i][r] = mu_rule(wr[g4 + i][r], f[i][r], e[i][r]);
       }
-      __builtin_amdgcn_sched_barrier(0);   // one group's loads in flight at a time
+      __builtin_amdgcn_sched_barrier(0);
     }
     // ---- stop bookkeeping (one thread), then every thread sees the new run flags ----
     if (tid == 0) {

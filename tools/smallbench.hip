@@ -80,6 +80,9 @@ int main(int argc, char** argv) {
   run(k_small_mu<16, 3, 2>, "no H update");
   run(k_small_mu<16, 3, 4>, "no h h^T / stop");
   run(k_small_mu<16, 3, 8>, "no F / E / W update");
+  run(k_small_mu<16, 3, 16>, "no E = W0 (h h^T)");
+  run(k_small_mu<16, 3, 32>, "W rule -> adds");
+  run(k_small_mu<16, 3, 48>, "no E, W rule -> adds");
   run(k_small_mu<16, 3, 15>, "barriers only");
   return 0;
 }
