@@ -133,6 +133,33 @@ struct GTile {
     return (uint32_t)(row * 128 + ((slot ^ ((row >> 1) & 7)) << 4));
   }
 
+  // the split form of compute(): fragments of one kk half of a stage, then its MFMAs
+  struct Frag {
+    d2 a[MB], b[NB];
+  };
+  __device__ __forceinline__ static void load_frag(const char* __restrict__ st, int kk, Frag& f) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int wr = w / WC, wc = w % WC;
+    const int fr = l & 15, g = l >> 4;
+    const char* sp = st + (wr * (RP / WR) + fr) * 128;
+    const char* sq = st + RP * 128 + (wc * (RQ / WC) + fr) * 128;
+    const int so = ((4 * kk + g) ^ (fr >> 1)) << 4;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) f.a[i] = *reinterpret_cast<const d2*>(sp + i * 16 * 128 + so);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) f.b[j] = *reinterpret_cast<const d2*>(sq + j * 16 * 128 + so);
+  }
+  __device__ __forceinline__ void mfma_frag(const Frag& f) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].x, f.b[j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].y, f.b[j].y, acc[i][j], 0, 0, 0);
+  }
+
   __device__ __forceinline__ void compute(const char* __restrict__ st) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int wr = w / WC, wc = w % WC;
@@ -234,7 +261,15 @@ struct GTile {
     wait_stages<D - 1, XL>(npro - 1, xl);
     step_barrier();
     int b = 0;
-    for (int s = 0; s < nst; ++s) {
+    // split steps: the kk = 1 MFMAs of stage s are issued AFTER the barrier that publishes stage s + 1,
+    // right behind the LDS reads of stage s + 1's kk = 0 fragments, so those reads (and the barrier) are
+    // covered by matrix work instead of leaving the pipe idle at every step.  Each accumulator still sees
+    // kk = 0 (x, y) then kk = 1 (x, y) of every stage in order: the same sums bit for bit.
+    // (the last step is peeled: no branch around the barrier, so the compiler's lgkmcnt for the kk = 1
+    // fragments leaves the next stage's reads in flight)
+    Frag f0, f1;
+    load_frag(smem, 0, f0);
+    for (int s = 0; s + 1 < nst; ++s) {
       if (s + D < nst) {
         const int bd = (b + D >= NBUF) ? b + D - NBUF : b + D;
         issue(base + bd * STAGE_BYTES, kbeg + (s + D) * BK2);
@@ -244,14 +279,25 @@ struct GTile {
         }
       }
       const char* cur = smem + b * STAGE_BYTES;
-      compute(cur);
+      load_frag(cur, 1, f1);
+      mfma_frag(f0);
       extra(cur);
-      if (s + 1 < nst) {
-        const int left = nst - s - 2;
-        wait_stages<D - 1, XL>(left < D - 1 ? left : D - 1, xl);
-        step_barrier();
-      }
-      b = (b + 1 == NBUF) ? 0 : b + 1;
+      const int bn = (b + 1 == NBUF) ? 0 : b + 1;
+      const int left = nst - s - 2;
+      __builtin_amdgcn_sched_barrier(0);   // the kk = 1 MFMAs stay behind the barrier and the next reads
+      wait_stages<D - 1, XL>(left < D - 1 ? left : D - 1, xl);
+      step_barrier();   // also: every wave has read stage s (its kk = 1 fragments are in registers)
+      load_frag(smem + bn * STAGE_BYTES, 0, f0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_frag(f1);
+      b = bn;
+    }
+    {   // last step (its DMA was issued D steps ago)
+      const char* cur = smem + b * STAGE_BYTES;
+      load_frag(cur, 1, f1);
+      mfma_frag(f0);
+      extra(cur);
+      mfma_frag(f1);
     }
     return true;
   }
