@@ -287,9 +287,19 @@ def main():
                          "launch; 'launches' counts the timed ones); kernels[*] with bound 'hbm': algorithmic bytes "
                          "per launch / mean duration vs 8 TB/s"),
                 "timing_stride": args.timing_stride}
-        tp = pmc_profile_for(args.config, dom)
+        tp = pmc_profile_for(args.config)
         if tp:
-            roof["traffic"], roof["traffic_unit"] = tp
+            per, src = tp
+            note = (f"HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, {src}, same kernel source), "
+                    "averaged over every launch of one C3 sweep like `achieved`")
+            if dom in per:
+                roof["traffic"], roof["traffic_unit"] = per[dom], note
+            for kname, b in per.items():
+                if kname in kernels:
+                    kr = kernels[kname]
+                    kr["traffic_bytes_per_launch"] = b
+                    kr["traffic_gbs"] = b / (kr["avg_ms"] * 1e-3) / 1e9
+                    kr["traffic_frac_hbm"] = kr["traffic_gbs"] / HBM_PEAK_GBS
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -388,27 +398,34 @@ def side_kernels(A_dev, m, n, k, reps=3):
     return out
 
 
-def pmc_profile_for(config, dom):
-    """HBM bytes per launch of the dominant kernel from the newest committed PMC passes (tools/profile_round.sh:
-    FETCH_SIZE x 2 + WRITE_SIZE) -- used only when the profile was taken on THIS kernel source (its recorded
-    source hash matches), so the figure cannot go stale silently."""
+PMC_NAMES = {"wta": ("k_wta2", "k_wta_narrow"), "ahtw": ("k_ahtw4",), "hupdate": ("k_hupdate",),
+             "labels": ("k_labels",), "counts": ("k_counts",)}
+
+
+def pmc_profile_for(config):
+    """HBM bytes per launch of the engine kernels from the newest committed PMC passes (tools/profile_round.sh:
+    FETCH_SIZE x 2 + WRITE_SIZE, averaged over every launch of one C3 sweep like `achieved`; the variants of one
+    kernel pooled by launch count) -- used only when the profile was taken on THIS kernel source (its recorded
+    source hash matches), so the figures cannot go stale silently.  Returns ({kernel: bytes}, source) or None."""
     from nmfconsensus_amd.build import source_sha256
 
     if config != "C3":
         return None
     import glob
     sha = source_sha256()
-    key = "k_wta2" if dom == "wta" else "k_ahtw4"
     for tp in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
         try:
             pm = json.load(open(tp))
         except Exception:
             continue
-        if pm.get("source_sha256") != sha or key not in pm:
+        if pm.get("source_sha256") != sha:
             continue
-        return (pm[key]["hbm_bytes_per_launch"],
-                "HBM bytes per launch, averaged over every launch of one C3 sweep like `achieved` (rocprofv3 "
-                f"FETCH_SIZE x2 + WRITE_SIZE, {os.path.relpath(tp, ROOT)}, same kernel source)")
+        per = {}
+        for k, names in PMC_NAMES.items():
+            rows = [pm[nm] for nm in names if nm in pm and pm[nm].get("launches")]
+            if rows:
+                per[k] = sum(r["hbm_bytes_per_launch"] * r["launches"] for r in rows) / sum(r["launches"] for r in rows)
+        return per, os.path.relpath(tp, ROOT)
     log("[bench] no committed PMC profile matches this kernel source: roofline.traffic = null")
     return None
 
