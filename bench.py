@@ -413,7 +413,7 @@ def pmc_profile_for(config):
         return None
     import glob
     sha = source_sha256()
-    for tp in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+    for tp in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_traffic.json"), recursive=True), reverse=True):
         try:
             pm = json.load(open(tp))
         except Exception:

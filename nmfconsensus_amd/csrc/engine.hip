@@ -122,6 +122,14 @@ enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID
 // restarts; panel count rounded up to a multiple of WTA_NPT (the large W^T A tile spans that many
 // panels).  Placement never changes a result bit (DESIGN.md "Determinism").
 constexpr int WTA_NPT = 4;
+#ifndef NMFC_AHTW_NBUF
+#define NMFC_AHTW_NBUF 2
+#endif
+#ifndef NMFC_AHTW_LATE
+#define NMFC_AHTW_LATE 1
+#endif
+constexpr int AHTW_NBUF = NMFC_AHTW_NBUF;          // LDS ring depth of the full-width A h^T tiles
+constexpr bool AHTW_LATE = NMFC_AHTW_LATE != 0;    // h h^T rows / W0 staged after the K loop (k_ahtw4 LATE)
 struct Packing {
   std::vector<RestartInfo> ri;   // active list, panel-contiguous
   std::vector<int> prb, pre;     // per panel: [begin, end) in ri
@@ -321,8 +329,7 @@ namespace {
 //   mid  2 panels x 128 samples, 8 waves,  96 KiB   1 / CU   1.0
 //   small 1 panel x  64 samples, 4 waves,  48 KiB   3 / CU   0.8
 //   tiny 1 panel x  32 samples, 4 waves,  36 KiB   4 / CU   0.6
-// Ties go to the larger tile.  A h^T uses 64-gene tiles only when the live panels' 128-gene tiles
-// would leave CUs idle.  Every shape accumulates in the canonical K order, so this never changes a bit.
+// Ties go to the larger tile.  A h^T uses 64-gene tiles only on small grids (below).  Every shape accumulates in the canonical K order, so this never changes a bit.
 struct TileChoice {
   int wta;          // 0 big, 3 mid, 1 small, 2 tiny
   bool ahtw_small;  // 64-gene A h^T tiles
@@ -348,7 +355,9 @@ TileChoice choose_tiles(const nmfc_engine* e, int np_live, int ntj) {
       tc.wta = c.id;
     }
   }
-  tc.ahtw_small = np * e->ngt < cu;
+  // 64-gene A h^T tiles (5 workgroups / CU) beat the 128-gene ones (3 / CU) only on grids of a few
+  // thousand tiles: R = 25 shard +3 %, R = 50 tied, R >= 100 128 genes ahead (tools/gpu_var_bench.sh)
+  tc.ahtw_small = np * e->ngt < 16 * cu;
   if (e->force_wta >= 0) tc.wta = e->force_wta;   // NMFC_WTA_TILE (tests: every shape gives the same bits)
   if (e->force_ahtw >= 0) tc.ahtw_small = e->force_ahtw == 1;
   return tc;
@@ -913,7 +922,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->W[cur].as<double>(), e->SHP.as<double>(), e->colinfo.as<ColInfo>(),
                                e->colact.as<int>(), nblk, 4 * e->ngt);
           } else {
-            auto ka = ahtw_small ? k_ahtw4<0, GT / 2> : k_ahtw4<0, GT>;
+            auto ka = ahtw_small ? k_ahtw4<0, GT / 2, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>
+                                 : k_ahtw4<0, GT, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>;
             hipLaunchKernelGGL(ka, dim3(grid_ahtw), dim3(256), 0, st, iter,
                                e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
                                e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), pk.npanels,

@@ -20,6 +20,7 @@ namespace nmfc {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef double d2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
 
 constexpr int PANEL = 64;          // restart columns per panel
 constexpr int BK = 32;             // padding multiple of the sample dimension (K of A h^T)
@@ -120,12 +121,14 @@ struct GTile {
 
   // DMA of the stage starting at K position k0 into the LDS buffer at byte address `buf`
   __device__ __forceinline__ void issue(uint32_t buf, int k0) const {
-    const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const uint32_t dst = buf + (uint32_t)(w + NW * i) * 1024u;
-      lds_dma16(i >= PPW_P ? rq : rp, dst, voff[i], k0 * 8);
-    }
+    for (int i = 0; i < PPW; ++i) issue_piece(buf, k0, i);
+  }
+  // piece i of this wave (the wave index is wave-uniform: read into an SGPR so M0 is scalar arithmetic)
+  __device__ __forceinline__ void issue_piece(uint32_t buf, int k0, int i) const {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t dst = buf + (uint32_t)(w + NW * i) * 1024u;
+    lds_dma16(i >= PPW_P ? rq : rp, dst, voff[i], k0 * 8);
   }
 
   // byte offset of (row, logical slot) in a stage
@@ -159,7 +162,6 @@ struct GTile {
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].y, f.b[j].y, acc[i][j], 0, 0, 0);
   }
-
   __device__ __forceinline__ void compute(const char* __restrict__ st) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int wr = w / WC, wc = w % WC;
@@ -270,6 +272,9 @@ struct GTile {
     Frag f0, f1;
     load_frag(smem, 0, f0);
     for (int s = 0; s + 1 < nst; ++s) {
+      const char* cur = smem + b * STAGE_BYTES;
+      // the stage's DMA pieces go out as one block at the step head (spreading them one by one between the
+      // MFMAs was measured 2 % slower on both contractions: the data then lands later)
       if (s + D < nst) {
         const int bd = (b + D >= NBUF) ? b + D - NBUF : b + D;
         issue(base + bd * STAGE_BYTES, kbeg + (s + D) * BK2);
@@ -278,7 +283,6 @@ struct GTile {
           xl = true;
         }
       }
-      const char* cur = smem + b * STAGE_BYTES;
       load_frag(cur, 1, f1);
       mfma_frag(f0);
       extra(cur);
@@ -792,9 +796,11 @@ __device__ __forceinline__ void ahtw_map(int item, int npanels, int ngt, int& p,
 
 // ---------------------------------------------------------------------------------------------
 // K3 v4 "ahtw4": F = A h^T on the GTile ring (NPT panels x GTG genes, 4 waves per panel: WR = NPT,
-// WC = 4, each wave 64 panel rows x GTG/4 genes) + the panels' h h^T rows in LDS.  NPT = 1, GTG = 128,
-// 3 stages: 72 + 8 KiB, two workgroups per CU; NPT = 2 halves the A-tile bytes per flop (one A tile feeds
-// two panels) at one workgroup of 8 waves per CU.  Column state lives in registers: each wave reads its
+// WC = 4, each wave 64 panel rows x GTG/4 genes) + the panels' h h^T rows in LDS.  Engine default (LATE,
+// NBUF = 2, GTG = 128): a 2 x 24 KiB ring and 160 VGPRs, so THREE workgroups share a CU and their K loops
+// cover each other's prologues and epilogues (MFMA busy 75.5 -> 80.2 % at full load, +4.5 % kernel rate
+// over the 3-stage, 80 KiB, two-per-CU form); the h h^T rows wait in registers until the loop is done,
+// and W0 streams in by 16-row blocks during the epilogue.  Column state lives in registers: each wave reads its
 // panel's 64 ColInfo entries (lane = column), the active set is a 64-bit ballot of colact[c] == iter
 // (k_hupdate stamps its restart's columns with the iteration it ran) and the E-operand rows' (lc0, k)
 // come by lane shuffles.  These setup loads are issued after the first DMA stages, so they overlap
@@ -807,22 +813,30 @@ __device__ __forceinline__ void ahtw_map(int item, int npanels, int ngt, int& p,
 // canonical GTile K order.
 // PR = 16 is the narrow (tail) form: only the first 16 columns of panel 0 are live, so the tile covers
 // those 16 rows (WC waves along the genes): a quarter of the H / W bytes and MFMA work per gene tile.
-template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4>
+// LATE: the h h^T rows stay in registers through the K loop and are staged afterwards into a ring buffer
+// the last step no longer reads, and W0 is loaded after the loop: no LDS beyond the ring and no W0
+// registers live in the loop, so more workgroups fit a CU (their K loops cover each other's epilogues).
+template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4, bool LATE = false>
+static constexpr int ahtw4_lds() {
+  return GTile<PR * NPT, GTG, NPT, WC, NBUF>::LDS_BYTES + (LATE ? 0 : NPT * PR * KMAX * 8);
+}
+template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4, bool LATE = false>
 static __global__ __launch_bounds__(64 * NPT * WC,
-                                    (GTile<PR * NPT, GTG, NPT, WC, NBUF>::LDS_BYTES + NPT * PR * KMAX * 8 <= 81920)
-                                        ? 2 * NPT * WC / 4
-                                        : NPT * WC / 4)
+                                    (163840 / ahtw4_lds<VARIANT, GTG, NBUF, NPT, PR, WC, LATE>()) * NPT * WC / 4 > 8
+                                        ? 8
+                                        : (163840 / ahtw4_lds<VARIANT, GTG, NBUF, NPT, PR, WC, LATE>()) * NPT * WC / 4)
 void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* __restrict__ Arm, long m_pad,
              double* __restrict__ W, const double* __restrict__ SHP, const ColInfo* __restrict__ ci,
              const int* __restrict__ colact, int npanels, int ngt) {
   using TileW4 = GTile<PR * NPT, GTG, NPT, WC, NBUF>;
   constexpr int AHTW4_SH = TileW4::LDS_BYTES;
-  constexpr int AHTW4_LDS = AHTW4_SH + NPT * PR * KMAX * 8;
+  constexpr int AHTW4_LDS = ahtw4_lds<VARIANT, GTG, NBUF, NPT, PR, WC, LATE>();
   static_assert(AHTW4_LDS <= 163840, "LDS of one CU");
   static_assert(PR == PANEL || (PR == 16 && NPT == 1), "narrow tiles: one 16-column block");
+  static_assert(!LATE || TileW4::STAGE_BYTES >= NPT * PR * KMAX * 8, "h h^T rows fit one ring stage");
   constexpr int NTH = 64 * NPT * WC;
   __shared__ __attribute__((aligned(1024))) char smem[AHTW4_LDS];
-  double* SHl = reinterpret_cast<double*>(smem + AHTW4_SH);
+  double* SHl = reinterpret_cast<double*>(smem + AHTW4_SH);   // !LATE; LATE: set after the K loop
   int pp, gt;
   ahtw_map(xcd_item(blockIdx.x, (npanels / NPT) * ngt), npanels / NPT, ngt, pp, gt);
   const int p0 = pp * NPT;   // first panel of the tile
@@ -832,10 +846,31 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
   uint64_t actmask = 0;
   TileW4 tl;
   tl.zero();
-  // PR = 16: the "panel" index p is a 16-column block (column 16 p of the stacked W / H)
-  const double* wsrc = W + (long)p * PR * m_pad + (long)gt * GTG + (GTG / WC) * wc + (lane & 15);
+  // PR = 16: the "panel" index p is a 16-column block (column 16 p of the stacked W / H).
+  // W0 loads and W stores through a buffer resource over this wave's W rows: one 32-bit lane offset, the
+  // (row block, nb) part wave-uniform in soffset -- no 64-bit row addresses held in VGPRs across the K loop
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      W + (long)p * PR * m_pad + (long)gt * GTG + (GTG / WC) * wc, 0, (int)(PR * m_pad * 8), 0x00020000);
+  const int wvoff = (int)(((lane >> 4) * m_pad + (lane & 15)) * 8);
+  auto woff = [&](int mb, int reg, int nb) { return (int)(((16 * mb + 4 * reg) * m_pad + 16 * nb) * 8); };
   double w0[TileW4::MB][TileW4::NB][4];
-  const bool live = tl.template run<TileW4::MB * TileW4::NB * 4>(
+  auto load_w0_block = [&](int mb) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+      for (int nb = 0; nb < TileW4::NB; ++nb)
+        w0[mb][nb][reg] = (VARIANT == 1 || VARIANT == 4)
+                              ? 1.0
+                              : __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rw, wvoff, woff(mb, reg, nb), 0));
+  };
+  auto load_w0 = [&] {
+#pragma unroll
+    for (int mb = 0; mb < TileW4::MB; ++mb) load_w0_block(mb);
+  };
+  constexpr int NSH = NPT * PR * KMAX / 2 / NTH;
+  static_assert(NSH * 2 * NTH == NPT * PR * KMAX, "h h^T rows split evenly over the threads");
+  d2 shv[NSH];
+  const bool live = tl.template run<LATE ? 0 : TileW4::MB * TileW4::NB * 4>(
       H + (long)p0 * PR * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
       [&] {   // setup loads, independent of each other, overlapping the first stages' DMA
         cc = lane < PR ? ci[(long)p * PR + lane] : ColInfo{0, 0, 0, 0};
@@ -843,9 +878,6 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
 #pragma unroll
         for (int q = 0; q < NPT; ++q) ca[q] = lane < PR ? colact[(long)(p0 + q) * PR + lane] : -1;
         const d2* src = reinterpret_cast<const d2*>(SHP + (long)p0 * PR * KMAX);
-        constexpr int NSH = NPT * PR * KMAX / 2 / NTH;
-        static_assert(NSH * 2 * NTH == NPT * PR * KMAX, "h h^T rows split evenly over the threads");
-        d2 shv[NSH];
 #pragma unroll
         for (int j = 0; j < NSH; ++j) shv[j] = src[tid + NTH * j];
         bool any = false;
@@ -856,28 +888,36 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
           any = any || mk != 0;
         }
         if (!any) return false;   // every panel of the tile idle (the same answer in every wave)
+        if constexpr (!LATE) {
 #pragma unroll
-        for (int j = 0; j < NSH; ++j) reinterpret_cast<d2*>(SHl)[tid + NTH * j] = shv[j];
+          for (int j = 0; j < NSH; ++j) reinterpret_cast<d2*>(SHl)[tid + NTH * j] = shv[j];
+        }
         return true;   // SHl is published by the ring prologue's barrier
       },
       [](const char*) {},
       [&] {
-#pragma unroll
-        for (int mb = 0; mb < TileW4::MB; ++mb)
-#pragma unroll
-          for (int reg = 0; reg < 4; ++reg)
-#pragma unroll
-            for (int nb = 0; nb < TileW4::NB; ++nb)
-              w0[mb][nb][reg] = (VARIANT == 1 || VARIANT == 4)
-                                    ? 1.0
-                                    : wsrc[(long)(16 * mb + (lane >> 4) + 4 * reg) * m_pad + 16 * nb];
+        if constexpr (!LATE) load_w0();
       });
   if (!live) return;
+  if constexpr (LATE) {
+    // the ring buffer of stage nst - 2: every wave passed the barrier after reading it (nst >= 2)
+    const int nst = (int)n_pad / BK2;
+    SHl = reinterpret_cast<double*>(smem + ((nst - 2) % NBUF) * TileW4::STAGE_BYTES);
+#pragma unroll
+    for (int j = 0; j < NSH; ++j) reinterpret_cast<d2*>(SHl)[tid + NTH * j] = shv[j];
+    // W0 by 16-row blocks, one block ahead of the epilogue's block loop (block mb's E reads blocks
+    // mb - 1 .. mb + 1 only), so at most three blocks are live at once
+#pragma unroll
+    for (int mb = 0; mb < (TileW4::MB < 2 ? TileW4::MB : 2); ++mb) load_w0_block(mb);
+    __syncthreads();
+  }
   if (actmask == 0) return;   // this wave's panel is idle (its partner panel is not)
-  double* wdst = W + (long)p * PR * m_pad + (long)gt * GTG + (GTG / WC) * wc + (lane & 15);
   const double* SHw = SHl + (long)wr * PR * KMAX;
 #pragma unroll
   for (int mb = 0; mb < TileW4::MB; ++mb) {
+    if constexpr (LATE) {
+      if (mb + 2 < TileW4::MB) load_w0_block(mb + 2);
+    }
     const int ra = 16 * mb + (lane & 15);
     const int alc = __shfl(cc.lc0, ra) & (PR - 1);   // tile-local (a restart never straddles a tile)
     const int ak = (VARIANT == 2 || VARIANT == 4 || !((actmask >> ra) & 1)) ? 0 : __shfl(cc.k, ra);
@@ -892,8 +932,10 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
     d4 e[TileW4::NB];
 #pragma unroll
     for (int nb = 0; nb < TileW4::NB; ++nb) e[nb] = d4{0.0, 0.0, 0.0, 0.0};
+    // K = the rows of the restarts touching block mb: within [16 mb - 15, 16 mb + 31) (k <= 16, restarts never
+    // leave the tile), i.e. K steps q in [4 mb - 4, 4 mb + 8)
 #pragma unroll
-    for (int q = 0; q < 4 * TileW4::MB; ++q) {   // K = the tile's rows (restarts never leave the tile)
+    for (int q = (4 * mb - 4 > 0 ? 4 * mb - 4 : 0); q < (4 * mb + 8 < 4 * TileW4::MB ? 4 * mb + 8 : 4 * TileW4::MB); ++q) {
       if (4 * q + 3 < lo || 4 * q >= hi) continue;   // wave-uniform
       const int bb = 4 * q + (lane >> 4) - alc;
       const double av = (bb >= 0 && bb < ak) ? SHw[ra * KMAX + bb] : 0.0;
@@ -908,7 +950,8 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
 #pragma unroll
       for (int nb = 0; nb < TileW4::NB; ++nb) {
         const double v = VARIANT == 4 ? tl.acc[mb][nb][reg] : mu_rule(w0[mb][nb][reg], tl.acc[mb][nb][reg], e[nb][reg]);
-        if (VARIANT != 3 || v == (double)iter * 1.5e300) wdst[(long)c * m_pad + 16 * nb] = v;
+        if (VARIANT != 3 || v == (double)iter * 1.5e300)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rw, wvoff, woff(mb, reg, nb), 0);
       }
     }
   }
