@@ -317,15 +317,18 @@ def test_narrow_end_kernels_bit_identical(oracle, golden, m, n, ks, R):
     runs = []
     try:
         os.environ["NMFC_SMALL"] = "0"   # keep the 1000 x 40 case on the batched kernels
-        for flag in ("1", "0"):
+        # narrow W^T A as the register-streaming kernel, as the LDS-ring kernel, and narrow forms disabled
+        for flag, stream in (("1", "1"), ("1", "0"), ("0", "1")):
             os.environ["NMFC_NARROW"] = flag
+            os.environ["NMFC_NARROW_STREAM"] = stream
             with Engine(A) as eng:
                 runs.append(eng.run(ks, R, maxiter=14, seed=3, stop_rule=0, want_factors=True))
     finally:
-        os.environ.pop("NMFC_NARROW", None)
-        os.environ.pop("NMFC_SMALL", None)
-    for j in range(len(ks) * R):
-        assert np.array_equal(runs[0].W[j], runs[1].W[j]) and np.array_equal(runs[0].H[j], runs[1].H[j]), j
+        for v in ("NMFC_NARROW", "NMFC_SMALL", "NMFC_NARROW_STREAM"):
+            os.environ.pop(v, None)
+    for run in runs[1:]:
+        for j in range(len(ks) * R):
+            assert np.array_equal(runs[0].W[j], run.W[j]) and np.array_equal(runs[0].H[j], run.H[j]), j
     k = ks[0]
     W0, H0 = oracle.init_restart(3, m, n, k)
     Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, 14, 0)
