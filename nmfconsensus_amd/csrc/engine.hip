@@ -136,6 +136,14 @@ constexpr int WTA_NPT = 4;
 #endif
 constexpr int NARROW_PF = NMFC_NARROW_PF;          // K steps in flight of the register-streaming narrow W^T A
 constexpr int NARROW_NBUF = NMFC_NARROW_NBUF;      // LDS ring depth of the narrow (tail) W^T A kernel
+#ifndef NMFC_WTA_MID_NBUF
+#define NMFC_WTA_MID_NBUF 3
+#endif
+#ifndef NMFC_WTA_MID_MINW
+#define NMFC_WTA_MID_MINW 1
+#endif
+constexpr int WTA_MID_NBUF = NMFC_WTA_MID_NBUF;    // ring depth of the 2-panel W^T A tile
+constexpr int WTA_MID_MINW = NMFC_WTA_MID_MINW;    // its launch-bounds waves per SIMD (4: two workgroups per CU)
 constexpr int AHTW_NBUF = NMFC_AHTW_NBUF;          // LDS ring depth of the full-width A h^T tiles
 constexpr bool AHTW_LATE = NMFC_AHTW_LATE != 0;    // h h^T rows / W0 staged after the K loop (k_ahtw4 LATE)
 struct Packing {
@@ -894,7 +902,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                sw_total);
           } else if (wta_mid) {   // npanels is a multiple of WTA_NPT, so of 2
             const int ng = pk.npanels / 2;
-            auto kw = (ntj >= 2) ? k_wta2<2, 128, 4, 2, 1> : k_wta2<2, 128, 4, 2, 2>;
+            auto kw = (ntj >= 2) ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW>
+                                 : k_wta2<2, 128, 4, 2, 2, WTA_MID_NBUF, WTA_MID_MINW>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
                                e->Acm.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),

@@ -62,6 +62,10 @@ __device__ __forceinline__ int xcd_item(int b, int nblocks) {
 // ---------------------------------------------------------------------------------------------
 constexpr int BK2 = 16;
 constexpr int GT_NBUF = 3;
+#ifndef NMFC_GT_PRIO
+#define NMFC_GT_PRIO 0
+#endif
+constexpr bool GT_PRIO = NMFC_GT_PRIO != 0;   // raise the wave priority around each MFMA block (experiment)
 
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, uint32_t lds_addr, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(uintptr_t)lds_addr, 16, voff,
@@ -153,6 +157,11 @@ struct GTile {
     for (int j = 0; j < NB; ++j) f.b[j] = *reinterpret_cast<const d2*>(sq + j * 16 * 128 + so);
   }
   __device__ __forceinline__ void mfma_frag(const Frag& f) {
+    if constexpr (GT_PRIO) __builtin_amdgcn_s_setprio(1);
+    mfma_frag_body(f);
+    if constexpr (GT_PRIO) __builtin_amdgcn_s_setprio(0);
+  }
+  __device__ __forceinline__ void mfma_frag_body(const Frag& f) {
 #pragma unroll
     for (int i = 0; i < MB; ++i)
 #pragma unroll
@@ -366,8 +375,8 @@ __device__ __forceinline__ bool panel_live(const int* __restrict__ prb, const in
 // samples; waves WR x WC.  Gram blocks (per panel: 4 diagonal + 3 straddling 16x16 blocks) are spread
 // over the ntj sample-tile workgroups of the panel group and their waves.
 // ---------------------------------------------------------------------------------------------
-template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF>
-static __global__ __launch_bounds__(WR * WC * 64) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
+template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1>
+static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
                                                               long m_pad, int ngroups, int ntj, int nsplit, int kchunk,
                                                               const int* __restrict__ prb, const int* __restrict__ pre,
                                                               const RestartInfo* __restrict__ ri,
