@@ -131,11 +131,7 @@ constexpr int WTA_NPT = 4;
 #ifndef NMFC_NARROW_NBUF
 #define NMFC_NARROW_NBUF 16
 #endif
-#ifndef NMFC_NARROW_PF
-#define NMFC_NARROW_PF 8
-#endif
-constexpr int NARROW_PF = NMFC_NARROW_PF;          // K steps in flight of the register-streaming narrow W^T A
-constexpr int NARROW_NBUF = NMFC_NARROW_NBUF;      // LDS ring depth of the narrow (tail) W^T A kernel
+constexpr int NARROW_NBUF = NMFC_NARROW_NBUF;      // LDS ring depth of the narrow (tail) W^T A kernel (16: +2 % on the R = 25 shard)
 #ifndef NMFC_WTA_MID_NBUF
 #define NMFC_WTA_MID_NBUF 3
 #endif
@@ -308,7 +304,6 @@ struct nmfc_engine {
   int repack_div = 5;                     // repack after nact / repack_div stops (env NMFC_REPACK_DIV)
   bool narrow_ok = true;                  // narrow end-of-sweep kernels allowed (env NMFC_NARROW=0 disables)
   int narrow_maxb = 3;                    // narrow form up to this many 16-column blocks (env NMFC_NARROW_MAXB)
-  bool narrow_stream = NARROW_PF > 0;     // narrow W^T A: register-streaming kernel (env NMFC_NARROW_STREAM=0: LDS ring)
   bool small_ok = true;                   // small-shape persistent kernel allowed (env NMFC_SMALL=0 disables)
   DevBuf Acm, Arm;
   // per-run buffers (grow-only)
@@ -525,7 +520,6 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_NARROW")) e->narrow_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_NARROW_MAXB")) e->narrow_maxb = std::min(8, std::max(1, atoi(s)));
   if (const char* s = getenv("NMFC_SMALL")) e->small_ok = atoi(s) != 0;
-  if (const char* s = getenv("NMFC_NARROW_STREAM")) e->narrow_stream = NARROW_PF > 0 && atoi(s) != 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
     const std::string v(s);
     e->force_ahtw = v == "128" ? 0 : v == "64" ? 1 : -1;
@@ -880,17 +874,10 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           TimedLaunch tl(e, KID_WTA, iter % e->timing_stride == 0);
           if (narrow) {
             const int ntq = (int)(e->n_cols_pad / 16);
-            if (e->narrow_stream) {   // register-streaming form (bit-identical to k_wta_narrow)
-              const int nw = e->nsplit * nblk * ntq;
-              hipLaunchKernelGGL((k_wta_stream<NARROW_PF>), dim3((nw + 3) / 4), dim3(256), 0, st, e->W[cur].as<double>(),
-                                 e->Acm.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk, e->colinfo.as<ColInfo>(),
-                                 e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
-            } else {
-              hipLaunchKernelGGL((k_wta_narrow<16, NARROW_NBUF>), dim3(e->nsplit * nblk * ntq), dim3(64), 0, st,
-                                 e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
-                                 e->colinfo.as<ColInfo>(),
-                                 e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
-            }
+            hipLaunchKernelGGL((k_wta_narrow<16, NARROW_NBUF>), dim3(e->nsplit * nblk * ntq), dim3(64), 0, st,
+                               e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
+                               e->colinfo.as<ColInfo>(),
+                               e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
             auto kw = (ntj >= 4) ? k_wta2<WTA_NPT, 128, 4, 2, 1> : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2>

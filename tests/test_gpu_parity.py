@@ -317,14 +317,12 @@ def test_narrow_end_kernels_bit_identical(oracle, golden, m, n, ks, R):
     runs = []
     try:
         os.environ["NMFC_SMALL"] = "0"   # keep the 1000 x 40 case on the batched kernels
-        # narrow W^T A as the register-streaming kernel, as the LDS-ring kernel, and narrow forms disabled
-        for flag, stream in (("1", "1"), ("1", "0"), ("0", "1")):
+        for flag in ("1", "0"):
             os.environ["NMFC_NARROW"] = flag
-            os.environ["NMFC_NARROW_STREAM"] = stream
             with Engine(A) as eng:
                 runs.append(eng.run(ks, R, maxiter=14, seed=3, stop_rule=0, want_factors=True))
     finally:
-        for v in ("NMFC_NARROW", "NMFC_SMALL", "NMFC_NARROW_STREAM"):
+        for v in ("NMFC_NARROW", "NMFC_SMALL"):
             os.environ.pop(v, None)
     for run in runs[1:]:
         for j in range(len(ks) * R):

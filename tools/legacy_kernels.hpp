@@ -790,4 +790,83 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw_p(int iter, const double
   }
 }
 
+// Round 2 experiment (not in the product: 73 us vs 66 us per narrow launch for the 16-stage LDS ring,
+// profiles/r02/narrow_stream_vs_lds_kstats.txt): the narrow W^T A with fragments streamed into registers.
+// ---------------------------------------------------------------------------------------------
+// K1 streaming form of the narrow tail (same outputs as k_wta_narrow, bit for bit): no LDS and no
+// barriers -- each wave owns one (chunk, 16-row block, 16-sample block) and loads its MFMA fragments
+// straight from global memory (buffer loads, 16 B per lane) PF K-steps ahead in a register ring.  In the
+// tail at most a few waves share a SIMD, so a wave's throughput is set by how many loads it keeps in
+// flight, not by LDS reuse: PF steps of 4 MFMAs cover PF x 256 matrix cycles of load latency.  The
+// fragments are exactly GTile's: lane (fr, g) holds K = 8 kk + 2 g + {x, y} of row fr, and each
+// accumulator sees kk = 0 (x, y) then kk = 1 (x, y) of every 16-K step in order (the canonical order).
+// ---------------------------------------------------------------------------------------------
+template <int PF>
+static __global__ __launch_bounds__(256) void k_wta_stream(const double* __restrict__ W, const double* __restrict__ Acm,
+                                                           long m_pad, int ntq, int nsplit, int kchunk, int nblk,
+                                                           const ColInfo* __restrict__ ci, double* __restrict__ Gpart,
+                                                           long g_ld, long g_split, double* __restrict__ SWpart,
+                                                           long sw_total) {
+  const int nw = nsplit * nblk * ntq;
+  const int item = xcd_item(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);   // 4 consecutive items per CU
+  if (item >= nw) return;
+  const int t = item % ntq, bk = (item / ntq) % nblk, s = item / (ntq * nblk);
+  const int kbeg = s * kchunk;
+  const int nst = (int)((min((long)kbeg + kchunk, m_pad) - kbeg) / BK2);
+  const int l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
+  const bool gram = t == 0;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(W + (long)bk * 16 * m_pad + kbeg), 0, (int)(16 * m_pad * 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(Acm + (long)t * 16 * m_pad + kbeg), 0, (int)(16 * m_pad * 8), 0x00020000);
+  const int voff = (int)((fr * m_pad + 2 * g) * 8);
+  d2 fa[PF][2], fb[PF][2];
+  auto load = [&](int u, int st) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      fa[u][kk] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(ra, voff, (st * BK2 + 8 * kk) * 8, 0));
+      fb[u][kk] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rb, voff, (st * BK2 + 8 * kk) * 8, 0));
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < nst) load(u, u);
+  d4 acc = (d4){0.0, 0.0, 0.0, 0.0}, gacc = (d4){0.0, 0.0, 0.0, 0.0};
+  for (int s0 = 0; s0 < nst; s0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      if (s0 + u < nst) {   // wave-uniform
+        const d2 a0 = fa[u][0], a1 = fa[u][1], b0 = fb[u][0], b1 = fb[u][1];
+        if (s0 + u + PF < nst) load(u, s0 + u + PF);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, b0.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, b0.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, b1.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, b1.y, acc, 0, 0, 0);
+        if (gram) {
+          gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, a0.x, gacc, 0, 0, 0);
+          gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, a0.y, gacc, 0, 0, 0);
+          gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, a1.x, gacc, 0, 0, 0);
+          gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, a1.y, gacc, 0, 0, 0);
+        }
+      }
+    }
+  }
+  double* out = Gpart + (long)s * g_split + (long)bk * 16 * g_ld + (long)t * 16;
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) out[(long)(g + 4 * reg) * g_ld + fr] = acc[reg];
+  if (gram) {
+    double* so = SWpart + (long)s * sw_total;
+    const ColInfo* cb = ci + (long)bk * 16;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int lr = g + 4 * reg, lcn = fr;
+      const ColInfo cr = cb[lr];
+      if (cr.k == 0 || cr.lc0 != cb[lcn].lc0 || cb[lcn].k == 0) continue;   // not the same restart
+      const int a = lr - (cr.lc0 & 15), b = lcn - (cr.lc0 & 15);
+      so[cr.sq_off + a * cr.k + b] = gacc[reg];
+      so[cr.sq_off + b * cr.k + a] = gacc[reg];
+    }
+  }
+}
+
 }  // namespace nmfc
