@@ -269,6 +269,13 @@ def main():
                 kr["tflops"] = fl / c / (avg_ms * 1e-3) / 1e12
                 kr["bound"] = "mfma"
                 kr["frac"] = kr["tflops"] / FP64_MFMA_PEAK_TFLOPS
+            elif kid == _lib.KID_COUNTS:
+                # R n^2 label compare-adds per k group (nmf.r:140-141): integer VALU work, not HBM traffic
+                ops = float(je - jb) * n * n
+                kr["int_ops_per_launch"] = ops
+                kr["gops"] = ops / (avg_ms * 1e-3) / 1e9
+                kr["bound"] = "valu (int32 compare + add; HBM bytes reported beside)"
+                kr["frac"] = None
             else:
                 kr["bound"] = "hbm"
                 kr["frac"] = kr["frac_hbm"]
@@ -368,6 +375,12 @@ def side_kernels(A_dev, m, n, k, reps=3):
     torch.cuda.synchronize()
     out = {}
     v, ms = ctypes.c_double(0.0), ctypes.c_double(0.0)
+    # one untimed call of each pass first: the first launch of a kernel loads its code object
+    L.nmfc_calculate_norm_dev(A_dev.data_ptr(), W.data_ptr(), H.data_ptr(), D.data_ptr(), m, n, k, ctypes.byref(v),
+                              ctypes.byref(ms))
+    M0.copy_(A_dev)
+    torch.cuda.synchronize()
+    L.nmfc_calculate_maxchange_dev(D.data_ptr(), M0.data_ptr(), m, n, 2.0 ** -26.5, ctypes.byref(v), ctypes.byref(ms))
     t = []
     for _ in range(reps):
         rc = L.nmfc_calculate_norm_dev(A_dev.data_ptr(), W.data_ptr(), H.data_ptr(), D.data_ptr(), m, n, k,

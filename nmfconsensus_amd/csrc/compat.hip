@@ -217,7 +217,18 @@ int nmfc_calculate_norm_dev(const double* da, const double* dw, const double* dh
   if (hipMalloc(&dp, blocks * 8) != hipSuccess) goto done;
   if (ms_out && (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess)) goto done;
   if (ms_out) (void)hipEventRecord(ev[0], 0);
-  hipLaunchKernelGGL(nmfc::k_norm_partial, dim3(gx, gy), dim3(nmfc::NT), 0, 0, da, dw, dh, dd, m, n, k, dp);
+  switch (k) {   // rank known at compile time up to KMAX (the engine's range); the generic pass above it
+#define NMFC_NORM_K(KK)                                                                                        \
+  case KK:                                                                                                    \
+    hipLaunchKernelGGL(nmfc::k_norm_partial_k<KK>, dim3(gx, gy), dim3(nmfc::NT), 0, 0, da, dw, dh, dd, m, n, dp); \
+    break;
+    NMFC_NORM_K(1) NMFC_NORM_K(2) NMFC_NORM_K(3) NMFC_NORM_K(4) NMFC_NORM_K(5) NMFC_NORM_K(6) NMFC_NORM_K(7)
+    NMFC_NORM_K(8) NMFC_NORM_K(9) NMFC_NORM_K(10) NMFC_NORM_K(11) NMFC_NORM_K(12) NMFC_NORM_K(13)
+    NMFC_NORM_K(14) NMFC_NORM_K(15) NMFC_NORM_K(16)
+#undef NMFC_NORM_K
+    default:
+      hipLaunchKernelGGL(nmfc::k_norm_partial, dim3(gx, gy), dim3(nmfc::NT), 0, 0, da, dw, dh, dd, m, n, k, dp);
+  }
   if (hipGetLastError() != hipSuccess) goto done;
   if (ms_out) (void)hipEventRecord(ev[1], 0);
   if (hipMemcpy(part.data(), dp, blocks * 8, hipMemcpyDeviceToHost) != hipSuccess) goto done;

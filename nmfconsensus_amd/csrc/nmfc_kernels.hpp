@@ -1607,6 +1607,61 @@ static __global__ __launch_bounds__(NT) void k_norm_partial(const double* __rest
   if (threadIdx.x == 0) partial[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
 }
 
+// The same pass for rank K <= 16 known at compile time: the thread's row of W is loaded once into
+// registers, the column of H is wave-uniform (scalar loads), and 4 columns are in flight per step, so the
+// pass streams A in and d out at HBM rate instead of re-reading W per element.  Per element the sum over
+// q runs in q order with fma, as k_norm_partial (identical d); the per-block partial of v^2 likewise.
+template <int K>
+static __global__ __launch_bounds__(NT) void k_norm_partial_k(const double* __restrict__ a, const double* __restrict__ w,
+                                                              const double* __restrict__ h, double* __restrict__ d, int m,
+                                                              int n, double* __restrict__ partial) {
+  __shared__ double red[NT];
+  const int i = blockIdx.x * NT + threadIdx.x;
+  double ss = 0.0;
+  if (i < m) {
+    double wr[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) wr[q] = w[i + (long)q * m];
+    constexpr int U = 4;
+    int j = blockIdx.y;
+    for (; j + (U - 1) * (int)gridDim.y < n; j += U * gridDim.y) {
+      double av[U], sv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) av[u] = a[(long)(j + u * gridDim.y) * m + i];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double* hc = h + (long)(j + u * gridDim.y) * K;
+        double sacc = 0.0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) sacc = fma(wr[q], hc[q], sacc);
+        sv[u] = sacc;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double v = av[u] - sv[u];
+        d[(long)(j + u * gridDim.y) * m + i] = v;
+        ss = fma(v, v, ss);
+      }
+    }
+    for (; j < n; j += gridDim.y) {
+      const double* hc = h + (long)j * K;
+      double sacc = 0.0;
+#pragma unroll
+      for (int q = 0; q < K; ++q) sacc = fma(wr[q], hc[q], sacc);
+      const double v = a[(long)j * m + i] - sacc;
+      d[(long)j * m + i] = v;
+      ss = fma(v, v, ss);
+    }
+  }
+  red[threadIdx.x] = ss;
+  __syncthreads();
+  for (int off = NT / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
+}
+
 static __global__ __launch_bounds__(NT) void k_maxchange_partial(const double* __restrict__ mat,
                                                                  double* __restrict__ mat0, long len,
                                                                  double* __restrict__ partial) {

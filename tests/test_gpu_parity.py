@@ -153,6 +153,20 @@ def test_norm_and_maxchange(golden):
     assert np.array_equal(m0, golden["maxchange_mat0_after"])
 
 
+@pytest.mark.parametrize("k", [1, 3, 10, 16, 20])
+def test_norm_rank_templated_pass(k):
+    """calculateNorm's rank-templated pass (k <= 16) and the generic pass (k > 16) against numpy: d = a - w h
+    per element with the q-ordered fma sum, the norm within 1e-12."""
+    from nmfconsensus_amd import libnmf
+    rng = np.random.default_rng(100 + k)
+    m, n = 3001, 151
+    a, w, h = rng.random((m, n)), rng.random((m, k)), rng.random((k, n))
+    v, d = libnmf.calculateNorm(np.asfortranarray(a), np.asfortranarray(w), np.asfortranarray(h))
+    ref = a - w @ h
+    assert relfro(d, ref) < 1e-13
+    assert abs(v - np.linalg.norm(ref) / np.sqrt(m * n)) <= 1e-12 * v
+
+
 def test_consensus_entry_matches_sweep(gct_engine, golden):
     from nmfconsensus_amd.nmf import computeConsensusMatrixFromClusterings
     k = 3
