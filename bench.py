@@ -137,6 +137,9 @@ def main():
     ap.add_argument("--stop-rule", default="ref_compat", choices=["fixed", "ref_compat", "argmax_stable"])
     ap.add_argument("--restarts", type=int, default=None, help="override R (restarts per k)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--groups", type=int, default=1, help="restart groups per GPU (engines on their own streams)")
+    ap.add_argument("--overlap-host", action="store_true",
+                    help="run each sweep's cophenetic step on a host thread beside the next sweep's GPU work")
     ap.add_argument("--cpu-iters", type=int, default=100, help="iterations per k in the CPU sample (~20 s wall on 16 cores)")
     ap.add_argument("--cpu-cores", type=int, default=None)
     ap.add_argument("--no-timing", action="store_true", help="disable per-launch HIP event timing")
@@ -188,28 +191,62 @@ def main():
     A_host = planted_matrix(m, n)
     A_dev = torch.from_numpy(A_host.T.copy()).to(dev)          # (n, m) row-major == (m, n) column-major
     torch.cuda.synchronize()
-    eng = Engine(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local)
-    counts = torch.zeros((nk, n, n), dtype=torch.int32, device=dev)
+    G = max(1, args.groups)
+    # G restart groups per GPU: one engine (own HIP stream, own buffers) per contiguous sub-shard of the
+    # rank's jobs, driven from G host threads, so the groups' launches interleave on the GPU
+    engs = [Engine(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local) for _ in range(G)]
+    eng = engs[0]
+    counts_g = [torch.zeros((nk, n, n), dtype=torch.int32, device=dev) for _ in range(G)]
+    counts = counts_g[0]
     jb, je = shard_range(nk * R, rank, world)
+    sub = [(jb + (je - jb) * g // G, jb + (je - jb) * (g + 1) // G) for g in range(G)]
     timing = not args.no_timing
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=G + 1)
+    host = ThreadPoolExecutor(max_workers=1)
+
+    def run_group(g):
+        b, e = sub[g]
+        return engs[g].run(ks, R, maxiter=args.maxiter, seed=123, stop_rule=stop_rule, job_begin=b, job_end=e,
+                           counts_device_ptr=counts_g[g].data_ptr(), check_every=16)
+
+    def rho_of(cons_host):   # cophenetic correlation per k (nmf.r:165-172), the k's on parallel host threads
+        r = cophenetic_batch(cons_host, symmetric=True)[0]
+        return {k: float(r[i]) for i, k in enumerate(ks)}
+
+    pending = [None]
 
     def step():
         torch.cuda.current_stream().synchronize()   # the previous all-reduce has finished reading counts
-        res = eng.run(ks, R, maxiter=args.maxiter, seed=123, stop_rule=stop_rule, job_begin=jb, job_end=je,
-                      counts_device_ptr=counts.data_ptr(), check_every=16)
+        if G == 1:
+            res = run_group(0)
+        else:
+            parts = list(pool.map(run_group, range(G)))
+            res = SweepMerge(parts)
+            for c in counts_g[1:]:
+                counts.add_(c)
         if world > 1:
             torch.distributed.all_reduce(counts, op=torch.distributed.ReduceOp.SUM)
         cons = counts.to(torch.float64) / R
         rho = {}
-        if rank == 0:   # cophenetic correlation per k (nmf.r:165-172), the k's on parallel host threads
-            r = cophenetic_batch(cons.cpu().numpy())[0]
-            rho = {k: float(r[i]) for i, k in enumerate(ks)}
+        if rank == 0:
+            cons_host = cons.cpu().numpy()
+            if args.overlap_host:   # the cophenetic step of this sweep runs beside the next sweep's GPU work
+                prev, pending[0] = pending[0], host.submit(rho_of, cons_host)
+                rho = prev.result() if prev is not None else {}
+            else:
+                rho = rho_of(cons_host)
         return res, rho
 
-    eng.set_timing(False)
+    for e in engs:
+        e.set_timing(False)
     for _ in range(args.warmup):
         step()
-    eng.set_timing(timing, args.timing_stride)
+    if pending[0] is not None:
+        pending[0].result()
+        pending[0] = None
+    for e in engs:
+        e.set_timing(timing, args.timing_stride)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -224,13 +261,17 @@ def main():
         last = (res, rho)
         iters_all.append(res.iters.copy())
         for kid, a in acc.items():
-            c, ms = eng.kernel_time(kid)
-            b, ab = eng.kernel_bytes(kid)
-            a[0] += c
-            a[1] += ms
-            a[2] += eng.kernel_flops(kid) * c
-            a[3] += b * c
-            a[4] += ab * c
+            for e in engs:
+                c, ms = e.kernel_time(kid)
+                b, ab = e.kernel_bytes(kid)
+                a[0] += c
+                a[1] += ms
+                a[2] += e.kernel_flops(kid) * c
+                a[3] += b * c
+                a[4] += ab * c
+    if pending[0] is not None:   # the last sweep's cophenetic step is inside the timed region
+        last = (last[0], pending[0].result())
+        pending[0] = None
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -345,9 +386,21 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    eng.close()
+    for e in engs:
+        e.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+class SweepMerge:
+    """The per-group SweepResults of one step, in job order (groups hold contiguous job ranges)."""
+
+    def __init__(self, parts):
+        import numpy as np
+        self.parts = parts
+        self.iters = np.concatenate([p.iters for p in parts])
+        self.seconds_total = max(p.seconds_total for p in parts)
+        self.seconds_iterate = max(p.seconds_iterate for p in parts)
 
 
 def metric_name(config, m, n, ks):
@@ -567,7 +620,8 @@ def bench_brunet(args, rank, world, local, dev):
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    eng.close()
+    for e in engs:
+        e.close()
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -305,7 +305,7 @@ struct nmfc_engine {
   bool narrow_ok = true;                  // narrow end-of-sweep kernels allowed (env NMFC_NARROW=0 disables)
   int narrow_maxb = 3;                    // narrow form up to this many 16-column blocks (env NMFC_NARROW_MAXB)
   bool small_ok = true;                   // small-shape persistent kernel allowed (env NMFC_SMALL=0 disables)
-  DevBuf Acm, Arm;
+  DevBuf Acm, Arm, Ablk;   // Acm: small-shape kernel only; Ablk: K-blocked A for W^T A (see k_layout_a)
   // per-run buffers (grow-only)
   DevBuf W[2], H[2], Gpart, SWpart, SH, SHP, colact, Hfin, Wfin;
   DevBuf rinfo, stop_iter, stop_reason, unchanged, classes, n_stopped, Hstat, Wsnap;
@@ -540,11 +540,15 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   }
   e->kchunk = (int)std::min<long>(kchunk, e->m_pad);
   e->nsplit = (int)((e->m_pad + e->kchunk - 1) / e->kchunk);
-  if (e->Acm.ensure(sizeof(double) * e->n_cols_pad * e->m_pad) || e->Arm.ensure(sizeof(double) * e->m_pad * e->n_pad)) {
+  // Acm (column-major, padded) feeds only the small-shape kernel; the general path's W^T A reads the K-blocked Ablk
+  const bool small_shape = e->m_pad <= 1024 && n <= 64;
+  if ((small_shape && e->Acm.ensure(sizeof(double) * e->n_cols_pad * e->m_pad)) ||
+      e->Ablk.ensure(sizeof(double) * e->n_cols_pad * e->m_pad) || e->Arm.ensure(sizeof(double) * e->m_pad * e->n_pad)) {
     nmfc_engine_destroy(e);
     return nullptr;
   }
-  if ((err = hipMemsetAsync(e->Acm.p, 0, e->Acm.bytes, e->st)) != hipSuccess) return fail("memset", err);
+  if (small_shape && (err = hipMemsetAsync(e->Acm.p, 0, e->Acm.bytes, e->st)) != hipSuccess) return fail("memset", err);
+  if ((err = hipMemsetAsync(e->Ablk.p, 0, e->Ablk.bytes, e->st)) != hipSuccess) return fail("memset", err);
   if ((err = hipMemsetAsync(e->Arm.p, 0, e->Arm.bytes, e->st)) != hipSuccess) return fail("memset", err);
   const double* dA = A;
   DevBuf tmp;
@@ -558,8 +562,10 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
     dA = tmp.as<double>();
   }
   dim3 grid((m + NT - 1) / NT, n);
-  hipLaunchKernelGGL(k_layout_a, grid, dim3(NT), 0, e->st, dA, (long)m, m, n, e->m_pad, e->n_pad, e->Acm.as<double>(),
-                     e->Arm.as<double>());
+  hipLaunchKernelGGL(k_layout_a, grid, dim3(NT), 0, e->st, dA, (long)m, m, n, e->m_pad, e->n_pad,
+                     small_shape ? e->Acm.as<double>() : nullptr, e->Arm.as<double>());
+  hipLaunchKernelGGL(k_layout_ablk, dim3((unsigned)((m + NT - 1) / NT), (unsigned)((n + 15) / 16)), dim3(NT), 0,
+                     e->st, dA, (long)m, m, n, e->n_cols_pad, e->Ablk.as<double>());
   if ((err = hipGetLastError()) != hipSuccess) return fail("k_layout_a", err);
   if ((err = hipStreamSynchronize(e->st)) != hipSuccess) return fail("sync", err);
   tmp.release();
@@ -571,7 +577,7 @@ void nmfc_engine_destroy(nmfc_engine* e) {
   if (e->st) (void)hipStreamSynchronize(e->st);
   drain_timing(e);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
-  DevBuf* bufs[] = {&e->Acm,       &e->Arm,       &e->W[0],      &e->W[1],     &e->H[0],       &e->H[1],
+  DevBuf* bufs[] = {&e->Acm,       &e->Arm,       &e->Ablk,      &e->W[0],      &e->W[1],     &e->H[0],       &e->H[1],
                     &e->Gpart,     &e->SWpart,    &e->SH,        &e->SHP,      &e->colact,     &e->Hfin,
                     &e->Wfin,      &e->rinfo,
                     &e->stop_iter, &e->stop_reason, &e->unchanged, &e->classes, &e->n_stopped, &e->prb,
@@ -874,40 +880,41 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           TimedLaunch tl(e, KID_WTA, iter % e->timing_stride == 0);
           if (narrow) {
             const int ntq = (int)(e->n_cols_pad / 16);
-            hipLaunchKernelGGL((k_wta_narrow<16, NARROW_NBUF>), dim3(e->nsplit * nblk * ntq), dim3(64), 0, st,
-                               e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
+            hipLaunchKernelGGL((k_wta_narrow<16, NARROW_NBUF, true>), dim3(e->nsplit * nblk * ntq), dim3(64), 0, st,
+                               e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
                                e->colinfo.as<ColInfo>(),
                                e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
-            auto kw = (ntj >= 4) ? k_wta2<WTA_NPT, 128, 4, 2, 1> : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2>
-                                                                            : k_wta2<WTA_NPT, 128, 4, 2, 4>;
+            auto kw = (ntj >= 4)   ? k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true>
+                      : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2, GT_NBUF, 1, true>
+                                   : k_wta2<WTA_NPT, 128, 4, 2, 4, GT_NBUF, 1, true>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
-                               e->Acm.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
+                               e->Ablk.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
                                e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
                                sw_total);
           } else if (wta_mid) {   // npanels is a multiple of WTA_NPT, so of 2
             const int ng = pk.npanels / 2;
-            auto kw = (ntj >= 2) ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW>
-                                 : k_wta2<2, 128, 4, 2, 2, WTA_MID_NBUF, WTA_MID_MINW>;
+            auto kw = (ntj >= 2) ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW, true>
+                                 : k_wta2<2, 128, 4, 2, 2, WTA_MID_NBUF, WTA_MID_MINW, true>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
-                               e->Acm.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
+                               e->Ablk.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
                                e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
                                sw_total);
           } else if (!wta_tiny) {
-            hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1>), dim3(e->nsplit * pk.npanels * 2 * ntj), dim3(256), 0, st,
-                               e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, pk.npanels, 2 * ntj, e->nsplit,
+            hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, GT_NBUF, 1, true>), dim3(e->nsplit * pk.npanels * 2 * ntj), dim3(256),
+                               0, st, e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, pk.npanels, 2 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
                                e->SWpart.as<double>(), sw_total);
           } else {   // few live panels: 1-panel x 32-sample tiles, two 16x16 blocks per wave (short chains);
                      // at most one live workgroup per CU: an 8-stage ring (more DMA in flight per CU, 96 KiB)
-            auto kw = (long)e->nsplit * live_panels(pk) * 4 * ntj <= e->ncu ? k_wta2<1, 32, 4, 1, 1, 8>
-                                                                             : k_wta2<1, 32, 4, 1, 1>;
+            auto kw = (long)e->nsplit * live_panels(pk) * 4 * ntj <= e->ncu ? k_wta2<1, 32, 4, 1, 1, 8, 1, true>
+                                                                             : k_wta2<1, 32, 4, 1, 1, GT_NBUF, 1, true>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * pk.npanels * 4 * ntj), dim3(256), 0, st,
-                               e->W[cur].as<double>(), e->Acm.as<double>(), e->m_pad, pk.npanels, 4 * ntj, e->nsplit,
+                               e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, pk.npanels, 4 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
                                e->SWpart.as<double>(), sw_total);

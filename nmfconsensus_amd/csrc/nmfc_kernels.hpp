@@ -83,7 +83,10 @@ __device__ __forceinline__ void step_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int RP, int RQ, int WR, int WC, int NBUF = GT_NBUF>
+// QBLK: the Q operand is K-blocked ([K/16][rows][16] doubles: one 16-gene block of every row
+// contiguous, `ldq` = the total row count), so a stage of a tile is ONE contiguous RQ x 128 B run instead
+// of RQ rows 8 * ldq bytes apart.  The same canonical K order either way.
+template <int RP, int RQ, int WR, int WC, int NBUF = GT_NBUF, bool QBLK = false>
 struct GTile {
   static_assert(NBUF >= 2 && NBUF <= 16, "ring of 2..16 stages");
   static constexpr int NW = WR * WC;
@@ -100,19 +103,22 @@ struct GTile {
   d4 acc[MB][NB];
   __amdgpu_buffer_rsrc_t rp, rq;
   int voff[PPW];
+  int qkm;   // QBLK: bytes between consecutive K positions' blocks / 8 (= 8 * total rows); else 8
 
-  // P rows are K-contiguous at P + row*ldp, Q rows at Q + row*ldq (doubles)
-  __device__ __forceinline__ void bind(const double* P, long ldp, const double* Q, long ldq) {
+  // P rows are K-contiguous at P + row*ldp, Q rows at Q + row*ldq (doubles); QBLK: Q + (k/16)*16*ldq + row*16
+  __device__ __forceinline__ void bind(const double* P, long ldp, const double* Q, long ldq, int kend) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(P), 0, (int)(RP * ldp * 8), 0x00020000);
-    rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Q), 0, (int)(RQ * ldq * 8), 0x00020000);
+    rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Q), 0, QBLK ? (int)((long)kend * ldq * 8) : (int)(RQ * ldq * 8),
+                                           0x00020000);
+    qkm = QBLK ? (int)ldq * 8 : 8;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int piece = w + NW * i;
       const bool isq = i >= PPW_P;
       const int row = (isq ? piece - RP / 8 : piece) * 8 + (l >> 3);
       const int slot = (l & 7) ^ ((row >> 1) & 7);
-      voff[i] = (int)((long)row * (isq ? ldq : ldp) * 8 + slot * 16);
+      voff[i] = (int)((long)row * (isq ? (QBLK ? 16 : ldq) : ldp) * 8 + slot * 16);
     }
   }
 
@@ -132,7 +138,10 @@ struct GTile {
   __device__ __forceinline__ void issue_piece(uint32_t buf, int k0, int i) const {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t dst = buf + (uint32_t)(w + NW * i) * 1024u;
-    lds_dma16(i >= PPW_P ? rq : rp, dst, voff[i], k0 * 8);
+    if (i >= PPW_P)
+      lds_dma16(rq, dst, voff[i], k0 * qkm);
+    else
+      lds_dma16(rp, dst, voff[i], k0 * 8);
   }
 
   // byte offset of (row, logical slot) in a stage
@@ -220,7 +229,7 @@ struct GTile {
   __device__ __forceinline__ bool run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
                                       int kbeg, int kend, char* __restrict__ smem, Pre pre, Extra extra, AtLast at_last) {
     const int nst = (kend - kbeg) / BK2;
-    bind(P, ldp, Q, ldq);
+    bind(P, ldp, Q, ldq, kend);
     const uint32_t base = (uint32_t)(uintptr_t)smem;
     if constexpr (NBUF == 2) {   // one stage in flight, issued after the barrier that freed its buffer
       issue(base, kbeg);
@@ -375,7 +384,7 @@ __device__ __forceinline__ bool panel_live(const int* __restrict__ prb, const in
 // samples; waves WR x WC.  Gram blocks (per panel: 4 diagonal + 3 straddling 16x16 blocks) are spread
 // over the ntj sample-tile workgroups of the panel group and their waves.
 // ---------------------------------------------------------------------------------------------
-template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1>
+template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1, bool ABLK = false>
 static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
                                                               long m_pad, int ngroups, int ntj, int nsplit, int kchunk,
                                                               const int* __restrict__ prb, const int* __restrict__ pre,
@@ -384,7 +393,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
                                                               const int* __restrict__ stop_iter, double* __restrict__ Gpart,
                                                               long g_ld, long g_split, double* __restrict__ SWpart,
                                                               long sw_total) {
-  using T = GTile<64 * NPT, RQ, WR, WC, NBUF>;
+  using T = GTile<64 * NPT, RQ, WR, WC, NBUF, ABLK>;
   constexpr int NCAND = 7 * NPT;
   __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES + 64];
   int* need = reinterpret_cast<int*>(smem + T::LDS_BYTES);
@@ -411,10 +420,12 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
     }
     need[threadIdx.x] = nd;
   }
-  const double* P = W + (long)pg * 64 * NPT * m_pad;
-  const double* Q = Acm + (long)t * RQ * m_pad;
+  // ABLK: Acm is K-blocked over all ntj * RQ sample rows.  Both operands are rebased to the chunk start, so the
+  // buffer offsets stay within one chunk (32-bit for any n_cols_pad up to 2^17).
   const int kbeg = s * kchunk;
   const int kend = (int)min((long)kbeg + kchunk, m_pad);
+  const long ldq = ABLK ? (long)ntj * RQ : m_pad;
+  const double* Q = ABLK ? Acm + (long)kbeg * ldq + (long)t * RQ * 16 : Acm + (long)t * RQ * m_pad + kbeg;
   T tl;
   tl.zero();
   d4 gacc[GPW];
@@ -440,7 +451,8 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
       gram = gram || my_need[x];
     }
   }
-  tl.run(P, m_pad, Q, m_pad, kbeg, kend, smem, [&](const char* stg) {
+  const double* P = W + (long)pg * 64 * NPT * m_pad + kbeg;
+  tl.run(P, m_pad, Q, ldq, 0, kend - kbeg, smem, [&](const char* stg) {
     if (!gram) return;
 #pragma unroll
     for (int x = 0; x < GPW; ++x) {
@@ -493,13 +505,13 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
 // bit-identical to every other shape.  Tile t == 0 of each (chunk, block) also forms the block's 16 x 16
 // Gram block (nmf_mu.c:176); no restart crosses a block, so that is every Gram entry of its restarts.
 // ---------------------------------------------------------------------------------------------
-template <int RQ, int NBUF>
+template <int RQ, int NBUF, bool ABLK = false>
 static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restrict__ W, const double* __restrict__ Acm,
                                                           long m_pad, int ntq, int nsplit, int kchunk, int nblk,
                                                           const ColInfo* __restrict__ ci, double* __restrict__ Gpart,
                                                           long g_ld, long g_split, double* __restrict__ SWpart,
                                                           long sw_total) {
-  using T = GTile<16, RQ, 1, 1, NBUF>;
+  using T = GTile<16, RQ, 1, 1, NBUF, ABLK>;
   __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES];
   const int item = xcd_item(blockIdx.x, nsplit * nblk * ntq);
   const int t = item % ntq, bk = (item / ntq) % nblk, s = item / (ntq * nblk);
@@ -510,7 +522,9 @@ static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restri
   T tl;
   tl.zero();
   d4 gacc = (d4){0.0, 0.0, 0.0, 0.0};
-  tl.run(W + (long)bk * 16 * m_pad, m_pad, Acm + (long)t * RQ * m_pad, m_pad, kbeg, kend, smem, [&](const char* stg) {
+  const long ldq = ABLK ? (long)ntq * RQ : m_pad;   // operands rebased to the chunk start (see k_wta2)
+  const double* Q = ABLK ? Acm + (long)kbeg * ldq + (long)t * RQ * 16 : Acm + (long)t * RQ * m_pad + kbeg;
+  tl.run(W + (long)bk * 16 * m_pad + kbeg, m_pad, Q, ldq, 0, kend - kbeg, smem, [&](const char* stg) {
     if (!gram) return;
     const char* pa = stg + fr * 128;
 #pragma unroll
@@ -1574,8 +1588,23 @@ static __global__ void k_layout_a(const double* __restrict__ A, long lda, int m,
   const int j = blockIdx.y;
   if (i >= m) return;
   const double v = A[(long)j * lda + i];
-  Acm[(long)j * m_pad + i] = v;
+  if (Acm) Acm[(long)j * m_pad + i] = v;
   Arm[i * n_pad + j] = v;
+}
+
+// A -> Ablk, the K-blocked operand of W^T A: Ablk[(i / 16) * ld * 16 + j * 16 + i % 16] (ld = n_cols_pad rows),
+// so the 16-gene block of a tile's sample rows is one contiguous run.  Block (x, y): NT genes x the 16
+// sample columns 16 y ..; lanes run along the genes of one column (16 doubles = 128 B contiguous).
+static __global__ __launch_bounds__(NT) void k_layout_ablk(const double* __restrict__ A, long lda, int m, int n, long ld,
+                                                           double* __restrict__ Ablk) {
+  const long i = (long)blockIdx.x * NT + threadIdx.x;   // gene
+  if (i >= m) return;
+  const long kb = i >> 4, r = i & 15;
+#pragma unroll 4
+  for (int jj = 0; jj < 16; ++jj) {
+    const int j = 16 * blockIdx.y + jj;
+    if (j < n) Ablk[kb * ld * 16 + (long)j * 16 + r] = A[(long)j * lda + i];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

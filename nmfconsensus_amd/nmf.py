@@ -293,12 +293,17 @@ def cophenetic(C: np.ndarray):
     return rho, order, merge, height
 
 
-def cophenetic_batch(Cs: np.ndarray, nthreads: int = 0):
+def cophenetic_batch(Cs: np.ndarray, nthreads: int = 0, symmetric: bool = False):
     """cophenetic() for a stack of consensus matrices (nk, n, n), the k's on parallel host threads.
+    symmetric=True: the caller guarantees Cs[q] == Cs[q].T (consensus matrices are), so the row-major
+    stack is passed as is (no column-major copy).
     Returns (rho[nk], order[nk, n] 1-based, merge[nk, n-1, 2], height[nk, n-1])."""
     Cs = np.asarray(Cs, dtype=np.float64)
     nk, n, _ = Cs.shape
-    flat = np.ascontiguousarray(np.transpose(Cs, (0, 2, 1)))   # each matrix column-major
+    if symmetric:
+        flat = np.ascontiguousarray(Cs)
+    else:
+        flat = np.ascontiguousarray(np.transpose(Cs, (0, 2, 1)))   # each matrix column-major
     rho = np.zeros(nk, dtype=np.float64)
     order = np.zeros((nk, n), dtype=np.int32)
     merge = np.zeros((nk, n - 1, 2), dtype=np.int32)

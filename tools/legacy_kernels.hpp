@@ -664,7 +664,7 @@ static __global__ __launch_bounds__(256, 2) void k_ahtw_p(int iter, const double
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         lds_dma16(rs, base + D * TL::STAGE_BYTES + (uint32_t)(wc + 4 * j) * 1024u, (wc + 4 * j) * 1024 + 16 * lane, 0);
-      tl.bind(H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad);
+      tl.bind(H + (long)p * PANEL * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, (int)n_pad);
 #pragma unroll
       for (int q = 0; q < D; ++q) tl.issue(base + q * TL::STAGE_BYTES, q * BK2);
       __builtin_amdgcn_sched_barrier(0);

@@ -114,6 +114,16 @@ int main(int argc, char** argv) {
     std::vector<double> sp((size_t)cols * KMAX, 1e-3);
     CK(hipMemcpy(SHP, sp.data(), sizeof(double) * sp.size(), hipMemcpyHostToDevice));
   }
+  // K-blocked copy of Acm: Ablk[kb][row][16] (one 16-gene block of every sample row contiguous)
+  double* Ablk;
+  CK(hipMalloc(&Ablk, sizeof(double) * n_cols_pad * m_pad));
+  {
+    std::vector<double> a((size_t)n_cols_pad * m_pad), b(a.size());
+    CK(hipMemcpy(a.data(), Acm, sizeof(double) * a.size(), hipMemcpyDeviceToHost));
+    for (long r = 0; r < n_cols_pad; ++r)
+      for (long k = 0; k < m_pad; ++k) b[(size_t)(k / 16) * n_cols_pad * 16 + r * 16 + (k % 16)] = a[(size_t)r * m_pad + k];
+    CK(hipMemcpy(Ablk, b.data(), sizeof(double) * b.size(), hipMemcpyHostToDevice));
+  }
   CK(hipMemset(SWpart, 0, sizeof(double) * nsplit * sw_total));
   CK(hipMemset(unch, 0, sizeof(int) * nall));
   CK(hipMemset(cls, 0, sizeof(int) * nall * 512));
@@ -153,6 +163,8 @@ int main(int argc, char** argv) {
            npanels, useful);
 #define WTA_ARGS                                                                                              \
   W, Acm, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, sw_total
+#define WTA_ARGS_B                                                                                            \
+  W, Ablk, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, sw_total
     auto report = [&](const char* name, float ms) {
       printf("  %-28s %8.4f ms  %6.1f TF\n", name, ms, useful / ms / 1e9);
     };
@@ -167,7 +179,31 @@ int main(int argc, char** argv) {
       report("wta2 tiny 1x32 nbuf8", timeit([&] {
                hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 8>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS);
              }, reps));
+      report("BLK wta2 tiny 1x32 nbuf3", timeit([&] {
+               hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 3, 1, true>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS_B);
+             }, reps));
+      report("BLK wta2 tiny 1x32 nbuf5", timeit([&] {
+               hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 5, 1, true>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS_B);
+             }, reps));
+      report("BLK wta2 tiny 1x32 nbuf8", timeit([&] {
+               hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 8, 1, true>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS_B);
+             }, reps));
+      {   // bit-identity of the blocked-A form
+        const size_t ng_ = (size_t)nsplit * g_split;
+        std::vector<double> g1(ng_), g2(ng_);
+        hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 3>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS);
+        CK(hipMemcpy(g1.data(), Gpart, ng_ * 8, hipMemcpyDeviceToHost));
+        CK(hipMemset(Gpart, 0, ng_ * 8));
+        hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 3, 1, true>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS_B);
+        CK(hipMemcpy(g2.data(), Gpart, ng_ * 8, hipMemcpyDeviceToHost));
+        size_t diff = 0;
+        for (size_t i = 0; i < ng_; ++i) diff += g1[i] != g2[i];
+        printf("  blocked-A vs row A: %zu of %zu G partial entries differ\n", diff, ng_);
+      }
       ntw = 2 * ntj;
+      report("BLK wta2 small 1x64 nbuf3", timeit([&] {
+               hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, 3, 1, true>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS_B);
+             }, reps));
       report("wta2 small 1x64 nbuf3", timeit([&] {
                hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, 3>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS);
              }, reps));
@@ -182,24 +218,42 @@ int main(int argc, char** argv) {
       report("wta2 mid 2x128 nbuf4", timeit([&] {
                hipLaunchKernelGGL((k_wta2<2, 128, 4, 2, 1, 4>), dim3(nsplit * ng * ntw), dim3(512), 0, 0, WTA_ARGS);
              }, reps));
+      report("BLK wta2 mid 2x128 nbuf3", timeit([&] {
+               hipLaunchKernelGGL((k_wta2<2, 128, 4, 2, 1, 3, 1, true>), dim3(nsplit * ng * ntw), dim3(512), 0, 0, WTA_ARGS_B);
+             }, reps));
       ng = npanels / 4;
       report("wta2 big 4x128 nbuf3", timeit([&] {
                hipLaunchKernelGGL((k_wta2<4, 128, 4, 2, 1, 3>), dim3(nsplit * ng * ntw), dim3(512), 0, 0, WTA_ARGS);
+             }, reps));
+      report("BLK wta2 big 4x128 nbuf3", timeit([&] {
+               hipLaunchKernelGGL((k_wta2<4, 128, 4, 2, 1, 3, 1, true>), dim3(nsplit * ng * ntw), dim3(512), 0, 0, WTA_ARGS_B);
              }, reps));
     }
     if (only && ri[nlive - 1].col0 + ri[nlive - 1].k <= 16) {   // narrow forms: live columns 0..15
       const int ntq = (int)(n_cols_pad / 16);
       report("wta narrow 16x16 nbuf4", timeit([&] {
                hipLaunchKernelGGL((k_wta_narrow<16, 4>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
-                                  kchunk, dci, Gpart, g_ld, g_split, SWpart, sw_total);
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("wta narrow 16x16 nbuf8", timeit([&] {
                hipLaunchKernelGGL((k_wta_narrow<16, 8>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
-                                  kchunk, dci, Gpart, g_ld, g_split, SWpart, sw_total);
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
+             }, reps));
+      report("BLK wta narrow 16x16 nbuf8", timeit([&] {
+               hipLaunchKernelGGL((k_wta_narrow<16, 8, true>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Ablk, m_pad, ntq, nsplit,
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
+             }, reps));
+      report("BLK wta narrow 16x16 nbuf16", timeit([&] {
+               hipLaunchKernelGGL((k_wta_narrow<16, 16, true>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Ablk, m_pad, ntq, nsplit,
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
+             }, reps));
+      report("wta narrow 16x16 nbuf16", timeit([&] {
+               hipLaunchKernelGGL((k_wta_narrow<16, 16>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("wta narrow 16x32 nbuf6", timeit([&] {
                hipLaunchKernelGGL((k_wta_narrow<32, 6>), dim3(nsplit * ntq / 2), dim3(64), 0, 0, W, Acm, m_pad, ntq / 2,
-                                  nsplit, kchunk, dci, Gpart, g_ld, g_split, SWpart, sw_total);
+                                  nsplit, kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
     }
     report("hupdate", timeit([&] {
