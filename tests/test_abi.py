@@ -162,3 +162,15 @@ def test_cophenetic_batch_equals_single():
         r1, o1, m1, h1 = cophenetic(Cs[q])
         assert rho[q] == r1 and np.array_equal(order[q], o1) and np.array_equal(merge[q], m1)
         assert np.array_equal(height[q], h1)
+
+def test_cophenetic_batch_symmetric_fast_path():
+    # consensus matrices are symmetric: the row-major stack passed as is gives the same results
+    from nmfconsensus_amd.nmf import cophenetic_batch
+    rng = np.random.default_rng(5)
+    n, nk = 47, 3
+    lab = rng.integers(0, 4, size=(nk, 25, n))
+    Cs = np.array([np.mean(l[:, :, None] == l[:, None, :], axis=0) for l in lab])
+    a = cophenetic_batch(Cs, nthreads=2)
+    b = cophenetic_batch(Cs, nthreads=2, symmetric=True)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)

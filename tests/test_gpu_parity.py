@@ -387,3 +387,37 @@ def test_small_path_agrees_with_batched_engine(golden):
     assert np.array_equal(a.counts, b.counts)
     for j in range(24):
         assert relfro(a.W[j], b.W[j]) < 1e-11 and relfro(a.H[j], b.H[j]) < 1e-11
+
+
+@pytest.mark.gpu
+def test_full_c3_sweep_properties():
+    # The full C3 shape (planted 20000 x 500, k = 2..10, reference stop rule) as a batched sweep, checked through
+    # size-independent properties (the oracle is too slow at this size for whole sweeps): every stop iteration is
+    # a check iteration >= 400 (200 unchanged checks, nmf_mu.c:253-271); labels = first argmax of the final H
+    # (nmf.r:128); counts = sum over restarts of label equality (nmf.r:140-141), symmetric with diagonal R; and the
+    # job-grid shards reproduce the whole sweep bit for bit (the multi-GPU split).
+    from nmfconsensus_amd.nmf import Engine
+    from nmfconsensus_amd.synthetic import planted_matrix
+    m, n, ks, R = 20000, 500, list(range(2, 11)), 2
+    A = planted_matrix(m, n)
+    with Engine(A) as eng:
+        full = eng.run(ks, R, maxiter=10000, seed=123, stop_rule=1, want_factors=True)
+        a = eng.run(ks, R, maxiter=10000, seed=123, stop_rule=1, job_begin=0, job_end=7, want_factors=True)
+        b = eng.run(ks, R, maxiter=10000, seed=123, stop_rule=1, job_begin=7, job_end=18, want_factors=True)
+    nj = len(ks) * R
+    assert np.all(full.iters >= 400) and np.all(full.iters % 2 == 0) and np.all(full.iters < 10000)
+    assert np.array_equal(a.counts + b.counts, full.counts)
+    assert np.array_equal(np.concatenate([a.iters, b.iters]), full.iters)
+    assert np.array_equal(np.concatenate([a.labels, b.labels]), full.labels)
+    for j in range(nj):
+        src, jj = (a, j) if j < 7 else (b, j - 7)
+        assert np.array_equal(src.H[jj], full.H[j]) and np.array_equal(src.W[jj], full.W[j])
+        Hj = full.H[j]
+        assert Hj.shape == (ks[j % len(ks)], n) and np.all(Hj >= 0)
+        assert np.array_equal(full.labels[j], np.argmax(Hj, axis=0) + 1)
+    for i, k in enumerate(ks):
+        lab = full.labels[i::len(ks)]
+        cnt = np.sum(lab[:, :, None] == lab[:, None, :], axis=0)
+        assert np.array_equal(full.counts[i], cnt)
+        assert np.array_equal(full.counts[i], full.counts[i].T) and np.all(np.diag(full.counts[i]) == R)
+        assert np.array_equal(full.consensus[i], full.counts[i] / R)
