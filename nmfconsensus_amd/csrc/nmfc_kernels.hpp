@@ -586,7 +586,10 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
                                              int* __restrict__ unchanged, int* __restrict__ classes, long cls_ld,
                                              int* __restrict__ n_stopped, double* __restrict__ SHP,
                                              int* __restrict__ colact, double* __restrict__ Hstat, HupdSmem& sm) {
-  constexpr int GS = (64 / K) < 1 ? 1 : (64 / K) > 16 ? 16 : (64 / K);
+#ifndef NMFC_HUPD_GSV   // chunk-partial values in flight per thread (32: 128 VGPRs, two workgroups per CU)
+#define NMFC_HUPD_GSV 32
+#endif
+  constexpr int GS = (NMFC_HUPD_GSV / K) < 1 ? 1 : (NMFC_HUPD_GSV / K) > 16 ? 16 : (NMFC_HUPD_GSV / K);
   double* sw = sm.sw;
   double* Hn = sm.Hn;
   double* win = sm.win;
@@ -716,7 +719,19 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
       const int cnt = min(HCH2, n - j0);
       const double* ha = Hn + pa * HCH2;
       const double* hb = Hn + pb * HCH2;
-      for (int q = pq; q < cnt; q += T) shacc = fma(ha[q], hb[q], shacc);
+      // 8 samples' operands loaded ahead of their (in-order) FMAs: the LDS latency is paid once per 8 terms
+      int q = pq;
+      for (; q + 7 * T < cnt; q += 8 * T) {
+        double xa[8], xb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          xa[u] = ha[q + u * T];
+          xb[u] = hb[q + u * T];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) shacc = fma(xa[u], xb[u], shacc);
+      }
+      for (; q < cnt; q += T) shacc = fma(ha[q], hb[q], shacc);
     }
   }
   shp[tid] = shacc;
@@ -768,7 +783,10 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
   }
 }
 
-static __global__ __launch_bounds__(NTH) void k_hupdate(int iter, int maxiter, int stop_rule,
+#ifndef NMFC_HUPD_MINW   // 4 waves per SIMD: two 512-thread workgroups per CU (full-load launch 150 -> 118 us)
+#define NMFC_HUPD_MINW 4
+#endif
+static __global__ __launch_bounds__(NTH, NMFC_HUPD_MINW) void k_hupdate(int iter, int maxiter, int stop_rule,
                                                         const RestartInfo* __restrict__ ri, int n, long n_pad,
                                                         const double* __restrict__ Gpart, long g_ld, long g_split,
                                                         int nsplit, const double* __restrict__ SWpart, long sw_total,
