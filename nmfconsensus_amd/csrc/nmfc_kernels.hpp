@@ -1,7 +1,8 @@
 // nmfc_kernels.hpp -- HIP kernels of the batched MU restart engine (gfx950 / CDNA4).
 //
 // Device layouts (DESIGN.md "Data layout in HBM"):
-//   Acm [n_cols_pad][m_pad]  column j of A, gene-contiguous              (operand of W^T A)
+//   Ablk [m_pad/16][n_cols_pad][16]  16-gene blocks of every column j of A (operand of W^T A)
+//   Acm [n_cols_pad][m_pad]  column j of A, gene-contiguous              (small-shape kernel only)
 //   Arm [m_pad][n_pad]       row i of A, sample-contiguous              (operand of A h^T)
 //   W   [cols][m_pad]        column c of the stacked W_all (restart owns columns col0..col0+k-1)
 //   H   [cols][n_pad]        row c of the stacked H_all (sample-contiguous)
