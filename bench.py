@@ -620,8 +620,7 @@ def bench_brunet(args, rank, world, local, dev):
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    for e in engs:
-        e.close()
+    eng.close()
     if world > 1:
         torch.distributed.destroy_process_group()
 
