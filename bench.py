@@ -137,6 +137,7 @@ def main():
     ap.add_argument("--stop-rule", default="ref_compat", choices=["fixed", "ref_compat", "argmax_stable"])
     ap.add_argument("--restarts", type=int, default=None, help="override R (restarts per k)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check-every", type=int, default=4, help="MU iterations enqueued between stop polls")
     ap.add_argument("--groups", type=int, default=1, help="restart groups per GPU (engines on their own streams)")
     ap.add_argument("--overlap-host", action="store_true",
                     help="run each sweep's cophenetic step on a host thread beside the next sweep's GPU work")
@@ -208,7 +209,7 @@ def main():
     def run_group(g):
         b, e = sub[g]
         return engs[g].run(ks, R, maxiter=args.maxiter, seed=123, stop_rule=stop_rule, job_begin=b, job_end=e,
-                           counts_device_ptr=counts_g[g].data_ptr(), check_every=16)
+                           counts_device_ptr=counts_g[g].data_ptr(), check_every=args.check_every)
 
     def rho_of(cons_host):   # cophenetic correlation per k (nmf.r:165-172), the k's on parallel host threads
         r = cophenetic_batch(cons_host, symmetric=True)[0]

@@ -52,7 +52,7 @@ typedef struct nmfc_sweep_opts {
   int max_init;
   int job_begin;      /* shard [job_begin, job_end) of the 0-based job list; job_end < 0 => all jobs */
   int job_end;
-  int check_every;    /* host polls the stopped-restart count every this many iterations (default 16) */
+  int check_every;    /* host polls the stopped-restart count every this many iterations (default 4) */
   int verbose;        /* 0 quiet; 1 per-sweep summary on stderr */
   double TolX;        /* NMFC_STOP_TOLX threshold (options_t.TolX, default 1e-4, setdefaultopts.c) */
   double TolFun;      /* NMFC_STOP_TOLX TolFun (default 1e-4) */

@@ -141,7 +141,7 @@ class Engine:
     def run(self, ks, R: int, *, maxiter: int = 10000, seed: int = 123, stop_rule: int = STOP_REF_COMPAT,
             label_rule: int = LABEL_ARGMAX, job_begin: int = 0, job_end: int = -1, W_init=None, H_init=None,
             want_factors: bool = False, want_counts: bool = True, counts_device_ptr: int | None = None,
-            check_every: int = 16, min_init: int = 0, max_init: int = 1, verbose: bool = False,
+            check_every: int = 4, min_init: int = 0, max_init: int = 1, verbose: bool = False,
             TolX: float = 1e-4, TolFun: float = 1e-4, init_stream: int = INIT_LIBNMF) -> SweepResult:
         ks = [int(k) for k in ks]
         nk = len(ks)
