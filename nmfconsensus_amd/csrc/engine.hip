@@ -871,7 +871,10 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       const int nblk = e->narrow_ok ? narrow_blocks(pk, e->narrow_maxb) : 0;
       const bool narrow = nblk > 0;
       const int ngt_ahtw = e->ngt * (ahtw_small ? 2 : 1);
-      const int grid_ahtw = pk.npanels * ngt_ahtw;
+      // panels holding restarts: the empty panels that pad the last 4-panel W^T A group get no A h^T
+      // workgroups (each would fetch a prologue stage before finding its panel idle) and no 1-panel W^T A ones
+      const int lp = std::max(1, live_panels(pk));
+      const int grid_ahtw = lp * ngt_ahtw;
       for (int c = 1; c <= chunk; ++c) {
         const int iter = it + c;
         {
@@ -896,7 +899,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
                                sw_total);
           } else if (wta_mid) {   // npanels is a multiple of WTA_NPT, so of 2
-            const int ng = pk.npanels / 2;
+            const int ng = (lp + 1) / 2;
             auto kw = (ntj >= 2) ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW, true>
                                  : k_wta2<2, 128, 4, 2, 2, WTA_MID_NBUF, WTA_MID_MINW, true>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
@@ -905,8 +908,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
                                sw_total);
           } else if (!wta_tiny) {
-            hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, GT_NBUF, 1, true>), dim3(e->nsplit * pk.npanels * 2 * ntj), dim3(256),
-                               0, st, e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, pk.npanels, 2 * ntj, e->nsplit,
+            hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, GT_NBUF, 1, true>), dim3(e->nsplit * lp * 2 * ntj), dim3(256),
+                               0, st, e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, lp, 2 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
                                e->SWpart.as<double>(), sw_total);
@@ -914,8 +917,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                      // at most one live workgroup per CU: an 8-stage ring (more DMA in flight per CU, 96 KiB)
             auto kw = (long)e->nsplit * live_panels(pk) * 4 * ntj <= e->ncu ? k_wta2<1, 32, 4, 1, 1, 8, 1, true>
                                                                              : k_wta2<1, 32, 4, 1, 1, GT_NBUF, 1, true>;
-            hipLaunchKernelGGL(kw, dim3(e->nsplit * pk.npanels * 4 * ntj), dim3(256), 0, st,
-                               e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, pk.npanels, 4 * ntj, e->nsplit,
+            hipLaunchKernelGGL(kw, dim3(e->nsplit * lp * 4 * ntj), dim3(256), 0, st,
+                               e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, lp, 4 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
                                e->SWpart.as<double>(), sw_total);
@@ -947,7 +950,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                  : k_ahtw4<0, GT, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>;
             hipLaunchKernelGGL(ka, dim3(grid_ahtw), dim3(256), 0, st, iter,
                                e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
-                               e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), pk.npanels,
+                               e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), lp,
                                ngt_ahtw);
           }
         }
