@@ -201,6 +201,8 @@ def main():
     # every kernel's HIP-event duration).
     jb, je = shard_range(nk * R, rank, world)
     G = args.groups if args.groups > 0 else (2 if (world > 1 and args.scaling == "strong" and je - jb >= 2) else 1)
+    if G > 8:
+        raise SystemExit(f"--groups {G}: at most 8 restart groups per GPU")
     engs = [Engine(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local) for _ in range(G)]
     eng = engs[0]
     counts_g = [torch.zeros((nk, n, n), dtype=torch.int32, device=dev) for _ in range(G)]

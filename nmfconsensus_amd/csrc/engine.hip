@@ -884,7 +884,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           TimedLaunch tl(e, KID_WTA, iter % e->timing_stride == 0);
           if (narrow) {
             const int ntq = (int)(e->n_cols_pad / 16);
-            hipLaunchKernelGGL((k_wta_narrow<16, NARROW_NBUF, true>), dim3(e->nsplit * nblk * ntq), dim3(64), 0, st,
+            hipLaunchKernelGGL((k_wta_narrow<16, NARROW_NBUF, true>), dim3(e->nsplit * nblk * (ntq + 1)), dim3(64), 0, st,
                                e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
                                e->colinfo.as<ColInfo>(),
                                e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);

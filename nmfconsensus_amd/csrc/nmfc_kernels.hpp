@@ -385,7 +385,9 @@ __device__ __forceinline__ bool panel_live(const int* __restrict__ prb, const in
 // samples; waves WR x WC.  Gram blocks (per panel: 4 diagonal + 3 straddling 16x16 blocks) are spread
 // over the ntj sample-tile workgroups of the panel group and their waves.
 // ---------------------------------------------------------------------------------------------
-template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1, bool ABLK = false>
+// GRAM = false: no Gram blocks (a probe: a wave carrying a Gram chain sets every barrier step of its workgroup,
+// 20-35 % of a 1-panel tile's time and 4-7 % of the 2- and 4-panel tiles', tools/tailbench.hip).
+template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1, bool ABLK = false, bool GRAM = true>
 static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
                                                               long m_pad, int ngroups, int ntj, int nsplit, int kchunk,
                                                               const int* __restrict__ prb, const int* __restrict__ pre,
@@ -449,7 +451,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
       my_need[x] = need[cand];
       my_ra[x] = 64 * q + 16 * br;
       my_rb[x] = 64 * q + 16 * bc;
-      gram = gram || my_need[x];
+      gram = GRAM && (gram || my_need[x]);
     }
   }
   const double* P = W + (long)pg * 64 * NPT * m_pad + kbeg;
@@ -506,6 +508,10 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
 // bit-identical to every other shape.  Tile t == 0 of each (chunk, block) also forms the block's 16 x 16
 // Gram block (nmf_mu.c:176); no restart crosses a block, so that is every Gram entry of its restarts.
 // ---------------------------------------------------------------------------------------------
+// Tile t == ntq of each (chunk, block) is the block's Gram item: its own wave runs the 16 x 16 W^T W block
+// (P = Q = the block's W rows) beside the W^T A waves, instead of a W^T A wave carrying the Gram chain next
+// to its own (that wave took 50 us where the others take 30).  A GTile MFMA with the same rows on both sides
+// is the in-tile Gram MFMA operand for operand, in the same canonical K order: bit-identical partials.
 template <int RQ, int NBUF, bool ABLK = false>
 static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restrict__ W, const double* __restrict__ Acm,
                                                           long m_pad, int ntq, int nsplit, int kchunk, int nblk,
@@ -513,34 +519,20 @@ static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restri
                                                           long g_ld, long g_split, double* __restrict__ SWpart,
                                                           long sw_total) {
   using T = GTile<16, RQ, 1, 1, NBUF, ABLK>;
+  using TG = GTile<16, 16, 1, 1, NBUF, false>;
+  static_assert(TG::LDS_BYTES <= T::LDS_BYTES, "the Gram item's ring fits the tile's");
   __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES];
-  const int item = xcd_item(blockIdx.x, nsplit * nblk * ntq);
-  const int t = item % ntq, bk = (item / ntq) % nblk, s = item / (ntq * nblk);
+  const int nt = ntq + 1;   // ntq W^T A tiles + the Gram item
+  const int item = xcd_item(blockIdx.x, nsplit * nblk * nt);
+  const int t = item % nt, bk = (item / nt) % nblk, s = item / (nt * nblk);
   const int kbeg = s * kchunk;
   const int kend = (int)min((long)kbeg + kchunk, m_pad);
   const int l = threadIdx.x, fr = l & 15, g = l >> 4;
-  const bool gram = t == 0;
-  T tl;
-  tl.zero();
-  d4 gacc = (d4){0.0, 0.0, 0.0, 0.0};
-  const long ldq = ABLK ? (long)ntq * RQ : m_pad;   // operands rebased to the chunk start (see k_wta2)
-  const double* Q = ABLK ? Acm + (long)kbeg * ldq + (long)t * RQ * 16 : Acm + (long)t * RQ * m_pad + kbeg;
-  tl.run(W + (long)bk * 16 * m_pad + kbeg, m_pad, Q, ldq, 0, kend - kbeg, smem, [&](const char* stg) {
-    if (!gram) return;
-    const char* pa = stg + fr * 128;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const d2 a = *reinterpret_cast<const d2*>(pa + (((4 * kk + g) ^ (fr >> 1)) << 4));
-      gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, a.x, gacc, 0, 0, 0);
-      gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, a.y, gacc, 0, 0, 0);
-    }
-  });
-  double* out = Gpart + (long)s * g_split + (long)bk * 16 * g_ld + (long)t * RQ;
-#pragma unroll
-  for (int nb = 0; nb < T::NB; ++nb)
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) out[(long)T::row_of(0, reg) * g_ld + T::col_of(nb)] = tl.acc[0][nb][reg];
-  if (gram) {
+  const double* Wb = W + (long)bk * 16 * m_pad + kbeg;
+  if (t == ntq) {   // the Gram item
+    TG tg;
+    tg.zero();
+    tg.run(Wb, m_pad, Wb, m_pad, 0, kend - kbeg, smem, [](const char*) {});
     double* so = SWpart + (long)s * sw_total;
     const ColInfo* cb = ci + (long)bk * 16;
 #pragma unroll
@@ -549,10 +541,21 @@ static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restri
       const ColInfo cr = cb[lr];
       if (cr.k == 0 || cr.lc0 != cb[lcn].lc0 || cb[lcn].k == 0) continue;   // not the same restart
       const int a = lr - (cr.lc0 & 15), b = lcn - (cr.lc0 & 15);
-      so[cr.sq_off + a * cr.k + b] = gacc[reg];
-      so[cr.sq_off + b * cr.k + a] = gacc[reg];
+      so[cr.sq_off + a * cr.k + b] = tg.acc[0][0][reg];
+      so[cr.sq_off + b * cr.k + a] = tg.acc[0][0][reg];
     }
+    return;
   }
+  T tl;
+  tl.zero();
+  const long ldq = ABLK ? (long)ntq * RQ : m_pad;   // operands rebased to the chunk start (see k_wta2)
+  const double* Q = ABLK ? Acm + (long)kbeg * ldq + (long)t * RQ * 16 : Acm + (long)t * RQ * m_pad + kbeg;
+  tl.run(Wb, m_pad, Q, ldq, 0, kend - kbeg, smem, [](const char*) {});
+  double* out = Gpart + (long)s * g_split + (long)bk * 16 * g_ld + (long)t * RQ;
+#pragma unroll
+  for (int nb = 0; nb < T::NB; ++nb)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) out[(long)T::row_of(0, reg) * g_ld + T::col_of(nb)] = tl.acc[0][nb][reg];
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -232,27 +232,27 @@ int main(int argc, char** argv) {
     if (only && ri[nlive - 1].col0 + ri[nlive - 1].k <= 16) {   // narrow forms: live columns 0..15
       const int ntq = (int)(n_cols_pad / 16);
       report("wta narrow 16x16 nbuf4", timeit([&] {
-               hipLaunchKernelGGL((k_wta_narrow<16, 4>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
+               hipLaunchKernelGGL((k_wta_narrow<16, 4>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
                                   kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("wta narrow 16x16 nbuf8", timeit([&] {
-               hipLaunchKernelGGL((k_wta_narrow<16, 8>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
+               hipLaunchKernelGGL((k_wta_narrow<16, 8>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
                                   kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("BLK wta narrow 16x16 nbuf8", timeit([&] {
-               hipLaunchKernelGGL((k_wta_narrow<16, 8, true>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Ablk, m_pad, ntq, nsplit,
+               hipLaunchKernelGGL((k_wta_narrow<16, 8, true>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Ablk, m_pad, ntq, nsplit,
                                   kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("BLK wta narrow 16x16 nbuf16", timeit([&] {
-               hipLaunchKernelGGL((k_wta_narrow<16, 16, true>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Ablk, m_pad, ntq, nsplit,
+               hipLaunchKernelGGL((k_wta_narrow<16, 16, true>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Ablk, m_pad, ntq, nsplit,
                                   kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("wta narrow 16x16 nbuf16", timeit([&] {
-               hipLaunchKernelGGL((k_wta_narrow<16, 16>), dim3(nsplit * ntq), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
+               hipLaunchKernelGGL((k_wta_narrow<16, 16>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
                                   kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("wta narrow 16x32 nbuf6", timeit([&] {
-               hipLaunchKernelGGL((k_wta_narrow<32, 6>), dim3(nsplit * ntq / 2), dim3(64), 0, 0, W, Acm, m_pad, ntq / 2,
+               hipLaunchKernelGGL((k_wta_narrow<32, 6>), dim3(nsplit * (ntq / 2 + 1)), dim3(64), 0, 0, W, Acm, m_pad, ntq / 2,
                                   nsplit, kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
     }
