@@ -907,17 +907,17 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
                                e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
                                sw_total);
-          } else if (!wta_tiny) {
-            hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, GT_NBUF, 1, true>), dim3(e->nsplit * lp * 2 * ntj), dim3(256),
+          } else if (!wta_tiny) {   // 1-panel tiles: the Gram blocks in 3 workgroups of their own per (chunk, panel)
+            hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, GT_NBUF, 1, true, true, true>), dim3(e->nsplit * lp * (2 * ntj + 3)), dim3(256),
                                0, st, e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, lp, 2 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
                                e->SWpart.as<double>(), sw_total);
           } else {   // few live panels: 1-panel x 32-sample tiles, two 16x16 blocks per wave (short chains);
                      // at most one live workgroup per CU: an 8-stage ring (more DMA in flight per CU, 96 KiB)
-            auto kw = (long)e->nsplit * live_panels(pk) * 4 * ntj <= e->ncu ? k_wta2<1, 32, 4, 1, 1, 8, 1, true>
-                                                                             : k_wta2<1, 32, 4, 1, 1, GT_NBUF, 1, true>;
-            hipLaunchKernelGGL(kw, dim3(e->nsplit * lp * 4 * ntj), dim3(256), 0, st,
+            auto kw = (long)e->nsplit * live_panels(pk) * 4 * ntj <= e->ncu ? k_wta2<1, 32, 4, 1, 1, 8, 1, true, true, true>
+                                                                             : k_wta2<1, 32, 4, 1, 1, GT_NBUF, 1, true, true, true>;
+            hipLaunchKernelGGL(kw, dim3(e->nsplit * lp * (4 * ntj + 3)), dim3(256), 0, st,
                                e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, lp, 4 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,

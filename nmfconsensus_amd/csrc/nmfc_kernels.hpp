@@ -104,11 +104,12 @@ struct GTile {
   d4 acc[MB][NB];
   __amdgpu_buffer_rsrc_t rp, rq;
   int voff[PPW];
-  int qkm;   // QBLK: bytes between consecutive K positions' blocks / 8 (= 8 * total rows); else 8
+  int qkm;
+  int wo = 0;   // wave offset: this tile's waves are wo .. wo + NW - 1 of the workgroup (several 1-wave tiles per workgroup)   // QBLK: bytes between consecutive K positions' blocks / 8 (= 8 * total rows); else 8
 
   // P rows are K-contiguous at P + row*ldp, Q rows at Q + row*ldq (doubles); QBLK: Q + (k/16)*16*ldq + row*16
   __device__ __forceinline__ void bind(const double* P, long ldp, const double* Q, long ldq, int kend) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int w = (threadIdx.x >> 6) - wo, l = threadIdx.x & 63;
     rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(P), 0, (int)(RP * ldp * 8), 0x00020000);
     rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Q), 0, QBLK ? (int)((long)kend * ldq * 8) : (int)(RQ * ldq * 8),
                                            0x00020000);
@@ -137,7 +138,7 @@ struct GTile {
   }
   // piece i of this wave (the wave index is wave-uniform: read into an SGPR so M0 is scalar arithmetic)
   __device__ __forceinline__ void issue_piece(uint32_t buf, int k0, int i) const {
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) - wo;
     const uint32_t dst = buf + (uint32_t)(w + NW * i) * 1024u;
     if (i >= PPW_P)
       lds_dma16(rq, dst, voff[i], k0 * qkm);
@@ -154,8 +155,8 @@ struct GTile {
   struct Frag {
     d2 a[MB], b[NB];
   };
-  __device__ __forceinline__ static void load_frag(const char* __restrict__ st, int kk, Frag& f) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __device__ __forceinline__ void load_frag(const char* __restrict__ st, int kk, Frag& f) const {
+    const int w = (threadIdx.x >> 6) - wo, l = threadIdx.x & 63;
     const int wr = w / WC, wc = w % WC;
     const int fr = l & 15, g = l >> 4;
     const char* sp = st + (wr * (RP / WR) + fr) * 128;
@@ -182,7 +183,7 @@ struct GTile {
       for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].y, f.b[j].y, acc[i][j], 0, 0, 0);
   }
   __device__ __forceinline__ void compute(const char* __restrict__ st) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int w = (threadIdx.x >> 6) - wo, l = threadIdx.x & 63;
     const int wr = w / WC, wc = w % WC;
     const int fr = l & 15, g = l >> 4;
     const char* sp = st + (wr * (RP / WR) + fr) * 128;
@@ -387,7 +388,11 @@ __device__ __forceinline__ bool panel_live(const int* __restrict__ prb, const in
 // ---------------------------------------------------------------------------------------------
 // GRAM = false: no Gram blocks (a probe: a wave carrying a Gram chain sets every barrier step of its workgroup,
 // 20-35 % of a 1-panel tile's time and 4-7 % of the 2- and 4-panel tiles', tools/tailbench.hip).
-template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1, bool ABLK = false, bool GRAM = true>
+// GITEM (1-panel tiles): the Gram blocks run in 3 extra workgroups per (chunk, panel), their first three waves
+// each one candidate block as a 1-wave GTile<16, 16> (P, Q = the block's W rows; the rest of the wave set exits),
+// beside the W^T A workgroups instead of on their waves (bit-identical: see k_wta_narrow).
+template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1, bool ABLK = false, bool GRAM = true,
+          bool GITEM = false>
 static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
                                                               long m_pad, int ngroups, int ntj, int nsplit, int kchunk,
                                                               const int* __restrict__ prb, const int* __restrict__ pre,
@@ -400,11 +405,49 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
   constexpr int NCAND = 7 * NPT;
   __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES + 64];
   int* need = reinterpret_cast<int*>(smem + T::LDS_BYTES);
-  const int nitems = nsplit * ngroups * ntj;
+  constexpr int NGW = GITEM ? 3 : 0;   // Gram workgroups per (chunk, panel)
+  const int ntt = ntj + NGW;
+  const int nitems = nsplit * ngroups * ntt;
   const int item = xcd_item(blockIdx.x, nitems);
-  const int t = item % ntj;
-  const int pg = (item / ntj) % ngroups;
-  const int s = item / (ntj * ngroups);
+  const int t = item % ntt;
+  const int pg = (item / ntt) % ngroups;
+  const int s = item / (ntt * ngroups);
+  if constexpr (GITEM) {
+    static_assert(NPT == 1 && T::NW >= 3, "Gram items: 1-panel tiles of at least 3 waves");
+    using TG = GTile<16, 16, 1, 1, NBUF, false>;
+    static_assert(3 * TG::LDS_BYTES <= T::LDS_BYTES, "three Gram rings fit the tile's");
+    if (t >= ntj) {
+      const int w = threadIdx.x >> 6, l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
+      const int x = 3 * (t - ntj) + w;   // candidate: 4 diagonal, 3 straddling blocks
+      if (w >= 3 || x >= 7) return;
+      if (!panel_live(prb, pre, pg, ri, stop_iter, 0)) return;
+      const int br = x < 4 ? x : x - 4, bc = x < 4 ? x : x - 3;
+      const ColInfo* cp = ci + (long)pg * PANEL;
+      if (br != bc) {   // a straddling block only when the restart at column 16 bc started before it
+        const ColInfo c = cp[16 * bc];
+        if (!(c.k > 0 && c.lc0 < 16 * bc)) return;
+      }
+      const int kbeg = s * kchunk;
+      const int kend = (int)min((long)kbeg + kchunk, m_pad);
+      TG tg;
+      tg.wo = w;
+      tg.zero();
+      const double* Pr = W + ((long)pg * PANEL + 16 * br) * m_pad + kbeg;
+      const double* Qr = W + ((long)pg * PANEL + 16 * bc) * m_pad + kbeg;
+      tg.run(Pr, m_pad, Qr, m_pad, 0, kend - kbeg, smem + w * TG::LDS_BYTES, [](const char*) {});
+      double* so = SWpart + (long)s * sw_total;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int lr = 16 * br + g + 4 * reg, lcn = 16 * bc + fr;
+        const ColInfo cr = cp[lr];
+        if (cr.k == 0 || cr.lc0 != cp[lcn].lc0 || cp[lcn].k == 0) continue;   // not the same restart
+        const int a = lr - cr.lc0, b = lcn - cr.lc0;
+        so[cr.sq_off + a * cr.k + b] = tg.acc[0][0][reg];
+        so[cr.sq_off + b * cr.k + a] = tg.acc[0][0][reg];
+      }
+      return;
+    }
+  }
   bool live[NPT];
   bool any = false;
 #pragma unroll
@@ -451,7 +494,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
       my_need[x] = need[cand];
       my_ra[x] = 64 * q + 16 * br;
       my_rb[x] = 64 * q + 16 * bc;
-      gram = GRAM && (gram || my_need[x]);
+      gram = GRAM && !GITEM && (gram || my_need[x]);
     }
   }
   const double* P = W + (long)pg * 64 * NPT * m_pad + kbeg;
