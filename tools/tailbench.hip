@@ -179,6 +179,25 @@ int main(int argc, char** argv) {
       report("wta2 tiny 1x32 nbuf8", timeit([&] {
                hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 8>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS);
              }, reps));
+      {   // 1-panel tiles with the Gram in workgroups of their own (the engine's tail form)
+        const int ntg = ntw + 3;
+        report("GIT wta2 tiny 1x32 nbuf3", timeit([&] {
+                 hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 3, 1, true, true, true>), dim3(nsplit * ng * ntg), dim3(256), 0, 0,
+                                    W, Ablk, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split,
+                                    SWpart, sw_total);
+               }, reps));
+        report("GIT wta2 tiny 1x32 nbuf8", timeit([&] {
+                 hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 8, 1, true, true, true>), dim3(nsplit * ng * ntg), dim3(256), 0, 0,
+                                    W, Ablk, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split,
+                                    SWpart, sw_total);
+               }, reps));
+        const int ntw2 = 2 * ntj, ntg2 = ntw2 + 3;
+        report("GIT wta2 small 1x64 nbuf3", timeit([&] {
+                 hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, 3, 1, true, true, true>), dim3(nsplit * ng * ntg2), dim3(256), 0, 0,
+                                    W, Ablk, m_pad, ng, ntw2, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split,
+                                    SWpart, sw_total);
+               }, reps));
+      }
       report("BLK wta2 tiny 1x32 nbuf3", timeit([&] {
                hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 3, 1, true>), dim3(nsplit * ng * ntw), dim3(256), 0, 0, WTA_ARGS_B);
              }, reps));
