@@ -146,12 +146,18 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=100, help="iterations per k in the CPU sample (~20 s wall on 16 cores)")
     ap.add_argument("--cpu-cores", type=int, default=None)
     ap.add_argument("--no-timing", action="store_true", help="disable per-launch HIP event timing")
-    ap.add_argument("--timing-stride", type=int, default=4,
-                    help="event-time the launches of every S-th MU iteration (a uniform sample; S=1 times all)")
+    ap.add_argument("--timing-stride", type=int, default=5,
+                    help="event-time the launches of every S-th MU iteration (S=1 times all; the default 5 is coprime "
+                         "to the stop-check parity and to the poll chunk, so the sample covers odd and even "
+                         "iterations and every position within a chunk)")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="strong (default): the fixed R restarts per k are split over the N GPUs (the north-star "
                          "job); weak: every GPU runs the full per-GPU workload (R restarts per k each, consensus "
                          "over R x N).  C4 is always weak (the per-GPU share of configs[3])")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="one-GPU replay of the N-GPU strong-scaling job: each of the N ranks' shard_range slices runs "
+                         "in turn on this GPU (as restart groups, the N > 1 policy); value = restarts / max shard time. "
+                         "A replay of the real shards, not a scaling curve (C3/C4 MU engine, one process)")
     ap.add_argument("--dump-iters", default=None, help="write the last step's per-job iteration counts (.npy)")
     ap.add_argument("--cpu-kind", default="reference", choices=["reference", "port"],
                     help="reference: the reference's own nmf_mu (oracle/_ref, fails loudly when absent); port: the "
@@ -171,14 +177,18 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from nmfconsensus_amd.synthetic import CONFIGS, planted_matrix
-    from nmfconsensus_amd.nmf import Engine, cophenetic_batch
-    from nmfconsensus_amd.distributed import shard_range
+    from nmfconsensus_amd.nmf import cophenetic_batch
+    from nmfconsensus_amd.distributed import RestartGroups, run_sharded_sweep, shard_range
     from nmfconsensus_amd import _lib
 
     if args.scaling is None:
         args.scaling = "weak" if args.config == "C4" else "strong"
     if args.config == "C5":
         return bench_brunet(args, rank, world, local, dev)
+    if args.simulate_world > 1:
+        if world > 1:
+            raise SystemExit("--simulate-world replays the shards in ONE process")
+        return bench_simulated_world(args, dev)
 
     m, n, ks, R, desc = CONFIGS[args.config]
     if args.config == "C4":
@@ -194,29 +204,19 @@ def main():
     A_host = planted_matrix(m, n)
     A_dev = torch.from_numpy(A_host.T.copy()).to(dev)          # (n, m) row-major == (m, n) column-major
     torch.cuda.synchronize()
-    # G restart groups per GPU: one engine (own HIP stream, own buffers) per contiguous sub-shard of the
-    # rank's jobs, driven from G host threads, so the groups' launches interleave on the GPU (+1 to +2.4 % at
-    # R = 25..200 per GPU).  Auto: 2 groups for a strong-scaling shard (N > 1), 1 for the
-    # whole job on one GPU, whose line is the per-kernel roofline measurement (overlapping groups stretch
-    # every kernel's HIP-event duration).
+    # G restart groups per GPU (distributed.RestartGroups: G engines on their own HIP streams over the same A,
+    # driven from G host threads, counts summed on the device; +1 to +2.4 % at R = 25..200 per GPU, DESIGN.md
+    # section 5).  Auto: 2 groups for a strong-scaling shard (N > 1), 1 for the whole job on one GPU, whose line
+    # is the per-kernel roofline measurement (overlapping groups stretch every kernel's HIP-event duration).
     jb, je = shard_range(nk * R, rank, world)
     G = args.groups if args.groups > 0 else (2 if (world > 1 and args.scaling == "strong" and je - jb >= 2) else 1)
     if G > 8:
         raise SystemExit(f"--groups {G}: at most 8 restart groups per GPU")
-    engs = [Engine(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local) for _ in range(G)]
-    eng = engs[0]
-    counts_g = [torch.zeros((nk, n, n), dtype=torch.int32, device=dev) for _ in range(G)]
-    counts = counts_g[0]
-    sub = [(jb + (je - jb) * g // G, jb + (je - jb) * (g + 1) // G) for g in range(G)]
+    groups = RestartGroups(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local, groups=G)
+    counts = torch.zeros((nk, n, n), dtype=torch.int32, device=dev)
     timing = not args.no_timing
     from concurrent.futures import ThreadPoolExecutor
-    pool = ThreadPoolExecutor(max_workers=G + 1)
     host = ThreadPoolExecutor(max_workers=1)
-
-    def run_group(g):
-        b, e = sub[g]
-        return engs[g].run(ks, R, maxiter=args.maxiter, seed=123, stop_rule=stop_rule, job_begin=b, job_end=e,
-                           counts_device_ptr=counts_g[g].data_ptr(), check_every=args.check_every)
 
     def rho_of(cons_host):   # cophenetic correlation per k (nmf.r:165-172), the k's on parallel host threads
         r = cophenetic_batch(cons_host, symmetric=True)[0]
@@ -225,16 +225,9 @@ def main():
     pending = [None]
 
     def step():
-        torch.cuda.current_stream().synchronize()   # the previous all-reduce has finished reading counts
-        if G == 1:
-            res = run_group(0)
-        else:
-            parts = list(pool.map(run_group, range(G)))
-            res = SweepMerge(parts)
-            for c in counts_g[1:]:
-                counts.add_(c)
-        if world > 1:
-            torch.distributed.all_reduce(counts, op=torch.distributed.ReduceOp.SUM)
+        # this rank's shard as G groups, counts into `counts`, RCCL SUM all-reduce when N > 1 (nmf.r:111-117)
+        _, res = run_sharded_sweep(groups, ks, R, rank=rank, world=world, counts_tensor=counts, maxiter=args.maxiter,
+                                   seed=123, stop_rule=stop_rule, check_every=args.check_every)
         cons = counts.to(torch.float64) / R
         rho = {}
         if rank == 0:
@@ -246,15 +239,13 @@ def main():
                 rho = rho_of(cons_host)
         return res, rho
 
-    for e in engs:
-        e.set_timing(False)
+    groups.set_timing(False)
     for _ in range(args.warmup):
         step()
     if pending[0] is not None:
         pending[0].result()
         pending[0] = None
-    for e in engs:
-        e.set_timing(timing, args.timing_stride)
+    groups.set_timing(timing, args.timing_stride)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -269,14 +260,8 @@ def main():
         last = (res, rho)
         iters_all.append(res.iters.copy())
         for kid, a in acc.items():
-            for e in engs:
-                c, ms = e.kernel_time(kid)
-                b, ab = e.kernel_bytes(kid)
-                a[0] += c
-                a[1] += ms
-                a[2] += e.kernel_flops(kid) * c
-                a[3] += b * c
-                a[4] += ab * c
+            for i, v in enumerate(groups.kernel_stats(kid)):
+                a[i] += v
     if pending[0] is not None:   # the last sweep's cophenetic step is inside the timed region
         last = (last[0], pending[0].result())
         pending[0] = None
@@ -339,7 +324,7 @@ def main():
                 "algo_bytes_per_launch": kernels[dom]["algo_bytes_per_launch"], "kernels": kernels,
                 "note": ("achieved = algorithmic flop per launch (SURVEY 8(d): 2mnk + 2mk^2 per live restart) / "
                          "the kernel's mean HIP-event duration over the timed launches of the timed sweeps (every "
-                         f"{args.timing_stride}th MU iteration's launches, a uniform sample, plus every labels/counts "
+                         f"{args.timing_stride}th MU iteration's launches, plus every labels/counts "
                          "launch; 'launches' counts the timed ones); kernels[*] with bound 'hbm': algorithmic bytes "
                          "per launch / mean duration vs 8 TB/s"),
                 "timing_stride": args.timing_stride}
@@ -399,21 +384,89 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    for e in engs:
-        e.close()
+    groups.close()
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
-class SweepMerge:
-    """The per-group SweepResults of one step, in job order (groups hold contiguous job ranges)."""
+def bench_simulated_world(args, dev):
+    """--simulate-world N: the N real shards of the strong-scaling job (distributed.shard_range over the
+    expand.grid job list, each as restart groups like an N > 1 rank) replayed one after another on this GPU.
+    A step = all N shards; the simulated N-GPU wall time of a step is its slowest shard, value = restarts /
+    that time (what N GPUs would deliver if each ran its shard at this GPU's speed; the all-reduce of 9 MB of
+    counts is not included).  The counts of all shards are summed and checked against a one-GPU sweep."""
+    import numpy as np
+    import torch
 
-    def __init__(self, parts):
-        import numpy as np
-        self.parts = parts
-        self.iters = np.concatenate([p.iters for p in parts])
-        self.seconds_total = max(p.seconds_total for p in parts)
-        self.seconds_iterate = max(p.seconds_iterate for p in parts)
+    from nmfconsensus_amd.distributed import RestartGroups, run_sharded_sweep
+    from nmfconsensus_amd.synthetic import CONFIGS, planted_matrix
+
+    W = args.simulate_world
+    m, n, ks, R, _ = CONFIGS[args.config]
+    if args.config == "C4":
+        R = R // 8
+    if args.restarts:
+        R = args.restarts
+    nk = len(ks)
+    stop_rule = {"fixed": 0, "ref_compat": 1, "argmax_stable": 2}[args.stop_rule]
+    A_dev = torch.from_numpy(planted_matrix(m, n).T.copy()).to(dev)
+    torch.cuda.synchronize()
+    G = args.groups if args.groups > 0 else 2
+    grp = RestartGroups(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=dev.index, groups=G)
+    part = torch.zeros((nk, n, n), dtype=torch.int32, device=dev)
+    total = torch.zeros_like(part)
+    shard_s = np.zeros((args.steps, W))
+    iters = []
+
+    def shard(r):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _, res = run_sharded_sweep(grp, ks, R, rank=r, world=W, counts_tensor=part, reduce=False,
+                                   maxiter=args.maxiter, seed=123, stop_rule=stop_rule, check_every=args.check_every)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, res
+
+    for _ in range(args.warmup):
+        for r in range(W):
+            shard(r)
+    for s_ in range(args.steps):
+        total.zero_()
+        its = []
+        for r in range(W):
+            shard_s[s_, r], res = shard(r)
+            total += part
+            its.append(res.iters)
+        iters = np.concatenate(its)
+    grp.close()
+    worst = shard_s.max(axis=1).mean()
+    value = nk * R / worst
+    # the sum of the shards' counts equals one whole sweep's (placement never changes a bit)
+    ref = RestartGroups(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=dev.index, groups=1)
+    whole = torch.zeros_like(part)
+    _, rw = run_sharded_sweep(ref, ks, R, rank=0, world=1, counts_tensor=whole, reduce=False, maxiter=args.maxiter,
+                              seed=123, stop_rule=stop_rule, check_every=args.check_every)
+    ref.close()
+    same = bool(torch.equal(whole, total)) and bool(np.array_equal(rw.iters, iters))
+    out = {
+        "metric": metric_name(args.config, m, n, ks) + f" [one-GPU replay of the {W}-GPU strong-scaling shards]",
+        "value": value, "unit": "restarts/s", "n_gpus": 1, "simulated_world": W, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": worst * 1e3, "higher_is_better": True, "scaling": "strong (simulated)",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (planted 4-group matrix, splitmix64 seed 20261015)",
+        "config": {"workload": f"{args.config}: synthetic {m}x{n} fp64, k={ks[0]}..{ks[-1]}, {R} restarts per k, "
+                               f"{nk * R} jobs split into {W} shard_range slices, {G} restart groups each",
+                   "per_gpu_restarts_per_s": value / W, "shard_seconds": shard_s.mean(axis=0).tolist(),
+                   "shard_jobs": [int(b - a) for a, b in (shard_range_(nk * R, r, W) for r in range(W))],
+                   "counts_equal_whole_sweep": same, "mean_iterations": float(iters.mean()),
+                   "max_iterations": int(iters.max())},
+    }
+    print(json.dumps(out), flush=True)
+    if not same:
+        raise SystemExit("simulated shards' counts differ from the whole sweep")
+
+
+def shard_range_(njobs, rank, world):
+    from nmfconsensus_amd.distributed import shard_range
+    return shard_range(njobs, rank, world)
 
 
 def metric_name(config, m, n, ks):
@@ -433,6 +486,7 @@ def side_kernels(A_dev, m, n, k, reps=3):
     from nmfconsensus_amd import _lib
 
     L = _lib.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream(A_dev.device).cuda_stream)   # the operands' producer stream
     g = torch.Generator(device=A_dev.device).manual_seed(7)
     W = torch.rand((k, m), dtype=torch.float64, device=A_dev.device, generator=g)   # (m x k) column-major
     H = torch.rand((n, k), dtype=torch.float64, device=A_dev.device, generator=g)   # (k x n) column-major
@@ -443,14 +497,14 @@ def side_kernels(A_dev, m, n, k, reps=3):
     v, ms = ctypes.c_double(0.0), ctypes.c_double(0.0)
     # one untimed call of each pass first: the first launch of a kernel loads its code object
     L.nmfc_calculate_norm_dev(A_dev.data_ptr(), W.data_ptr(), H.data_ptr(), D.data_ptr(), m, n, k, ctypes.byref(v),
-                              ctypes.byref(ms))
+                              ctypes.byref(ms), st)
     M0.copy_(A_dev)
     torch.cuda.synchronize()
-    L.nmfc_calculate_maxchange_dev(D.data_ptr(), M0.data_ptr(), m, n, 2.0 ** -26.5, ctypes.byref(v), ctypes.byref(ms))
+    L.nmfc_calculate_maxchange_dev(D.data_ptr(), M0.data_ptr(), m, n, 2.0 ** -26.5, ctypes.byref(v), ctypes.byref(ms), st)
     t = []
     for _ in range(reps):
         rc = L.nmfc_calculate_norm_dev(A_dev.data_ptr(), W.data_ptr(), H.data_ptr(), D.data_ptr(), m, n, k,
-                                       ctypes.byref(v), ctypes.byref(ms))
+                                       ctypes.byref(v), ctypes.byref(ms), st)
         if rc != 0:
             return {}
         t.append(ms.value)
@@ -463,7 +517,7 @@ def side_kernels(A_dev, m, n, k, reps=3):
         M0.copy_(A_dev)
         torch.cuda.synchronize()
         rc = L.nmfc_calculate_maxchange_dev(D.data_ptr(), M0.data_ptr(), m, n, 2.0 ** -26.5, ctypes.byref(v),
-                                            ctypes.byref(ms))
+                                            ctypes.byref(ms), st)
         if rc != 0:
             return out
         t.append(ms.value)
@@ -520,7 +574,7 @@ def bench_brunet(args, rank, world, local, dev):
     from nmfconsensus_amd.synthetic import CONFIGS, planted_matrix
     from nmfconsensus_amd.nmf import cophenetic
     from nmfconsensus_amd.brunet import BrunetEngine
-    from nmfconsensus_amd.distributed import shard_range
+    from nmfconsensus_amd.distributed import run_sharded_brunet, shard_range
     from nmfconsensus_amd import _lib
 
     m, n, ks, R, desc = CONFIGS["C5"]
@@ -539,10 +593,8 @@ def bench_brunet(args, rank, world, local, dev):
     timing = not args.no_timing
 
     def step():
-        res = eng.run(ks, R, maxiter=maxiter, seed=123456789, restart_begin=rb, restart_end=re,
-                      counts_device_ptr=counts.data_ptr())
-        if world > 1:
-            torch.distributed.all_reduce(counts, op=torch.distributed.ReduceOp.SUM)
+        _, res = run_sharded_brunet(eng, ks, R, rank=rank, world=world, counts_tensor=counts, maxiter=maxiter,
+                                    seed=123456789)
         cons = counts.to(torch.float64) / R
         rho = {}
         if rank == 0:

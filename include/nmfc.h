@@ -84,6 +84,8 @@ typedef struct nmfc_engine nmfc_engine;
  * a_on_device != 0: A is a device pointer (copied device-to-device into the engine's layouts). */
 nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a_on_device);
 void nmfc_engine_destroy(nmfc_engine* e);
+/* The HIP device ordinal the engine was created on (resolved at creation when device was -1); -1 for NULL. */
+int nmfc_engine_device(const nmfc_engine* e);
 
 void nmfc_default_opts(nmfc_sweep_opts* o);
 
@@ -145,6 +147,7 @@ typedef struct nmfc_brunet nmfc_brunet;
 void nmfc_brunet_default_opts(nmfc_brunet_opts* o);
 nmfc_brunet* nmfc_brunet_create(int device, const double* A, int m, int n, int a_on_device);
 void nmfc_brunet_destroy(nmfc_brunet* e);
+int nmfc_brunet_device(const nmfc_brunet* e);   /* as nmfc_engine_device */
 /* W_init/H_init (optional, host): every job of the shard in output order. Returns 0 or -1 (nmfc_last_error). */
 int nmfc_brunet_run(nmfc_brunet* e, const int* ks, int nk, int R, const nmfc_brunet_opts* opts, const double* W_init,
                     const double* H_init, nmfc_result* out);
@@ -156,11 +159,16 @@ long long nmfc_brunet_kernel_time(nmfc_brunet* e, int kernel_id, double* ms_out,
 /* calculateNorm (calculatenorm.c:44-78) and calculateMaxchange (calculatemaxchange.c:42-71) on
  * DEVICE-resident column-major operands (e.g. torch tensors) on the current HIP device: d = a - w h and
  * *norm_out = ||d||_F / sqrt(m n); *out = max|mat0 - mat| / (sqrteps + max|mat0|) with mat0 -= mat.
+ * stream: the hipStream_t (as void*) the operands were produced on; the pass and its partials buffer are
+ * ordered on it (NULL: the null stream), and the call returns after it has finished.
  * ms_out (may be NULL) receives the device time of the reduction pass.  Return 0, or -1 on failure. */
 int nmfc_calculate_norm_dev(const double* a, const double* w, const double* h, double* d, int m, int n, int k,
-                            double* norm_out, double* ms_out);
+                            double* norm_out, double* ms_out, void* stream);
 int nmfc_calculate_maxchange_dev(const double* mat, double* mat0, int m, int n, double sqrteps, double* out,
-                                 double* ms_out);
+                                 double* ms_out, void* stream);
+
+/* Frees the engine that nmf_mu (libnmf_compat.h) keeps across calls with the same A (its HBM and host copy). */
+void nmfc_nmf_mu_release(void);
 
 /* Diagnostics. */
 const char* nmfc_last_error(void);

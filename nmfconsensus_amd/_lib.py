@@ -56,10 +56,10 @@ EXPORTED = [
     "nmf_mu", "set_default_opts", "checkArguments", "checkMatrices", "randnumber", "generateMatrix",
     "calculateNorm", "calculateMaxchange",
     # include/nmfc.h
-    "nmfc_engine_create", "nmfc_engine_destroy", "nmfc_default_opts", "nmfc_engine_run", "nmfc_sweep",
+    "nmfc_engine_create", "nmfc_engine_destroy", "nmfc_engine_device", "nmfc_brunet_device", "nmfc_default_opts", "nmfc_engine_run", "nmfc_sweep",
     "nmfc_consensus", "nmfc_cophenetic", "nmfc_cophenetic_batch", "nmfc_cutree", "nmfc_last_error", "nmfc_version", "nmfc_engine_kernel_time",
     "nmfc_engine_set_timing", "nmfc_engine_kernel_flops", "nmfc_engine_kernel_bytes",
-    "nmfc_calculate_norm_dev", "nmfc_calculate_maxchange_dev",
+    "nmfc_calculate_norm_dev", "nmfc_calculate_maxchange_dev", "nmfc_nmf_mu_release",
     "nmfc_brunet_default_opts", "nmfc_brunet_create", "nmfc_brunet_destroy", "nmfc_brunet_run",
     "nmfc_brunet_set_timing", "nmfc_brunet_kernel_time",
 ]
@@ -103,6 +103,10 @@ def lib() -> ctypes.CDLL:
     L.nmfc_engine_create.restype = ctypes.c_void_p
     L.nmfc_engine_destroy.argtypes = [ctypes.c_void_p]
     L.nmfc_engine_destroy.restype = None
+    L.nmfc_engine_device.argtypes = [ctypes.c_void_p]
+    L.nmfc_engine_device.restype = c_int
+    L.nmfc_brunet_device.argtypes = [ctypes.c_void_p]
+    L.nmfc_brunet_device.restype = c_int
     L.nmfc_default_opts.argtypes = [ctypes.POINTER(SweepOpts)]
     L.nmfc_default_opts.restype = None
     L.nmfc_engine_run.argtypes = [ctypes.c_void_p, _ip, c_int, c_int, ctypes.POINTER(SweepOpts), _dp, _dp,
@@ -131,9 +135,11 @@ def lib() -> ctypes.CDLL:
     L.nmfc_engine_kernel_bytes.argtypes = [ctypes.c_void_p, c_int, _dp]
     L.nmfc_engine_kernel_bytes.restype = ctypes.c_double
     vp = ctypes.c_void_p
-    L.nmfc_calculate_norm_dev.argtypes = [vp, vp, vp, vp, c_int, c_int, c_int, _dp, _dp]
+    L.nmfc_calculate_norm_dev.argtypes = [vp, vp, vp, vp, c_int, c_int, c_int, _dp, _dp, vp]
     L.nmfc_calculate_norm_dev.restype = c_int
-    L.nmfc_calculate_maxchange_dev.argtypes = [vp, vp, c_int, c_int, ctypes.c_double, _dp, _dp]
+    L.nmfc_calculate_maxchange_dev.argtypes = [vp, vp, c_int, c_int, ctypes.c_double, _dp, _dp, vp]
+    L.nmfc_nmf_mu_release.argtypes = []
+    L.nmfc_nmf_mu_release.restype = None
     L.nmfc_calculate_maxchange_dev.restype = c_int
     L.nmfc_brunet_default_opts.argtypes = [ctypes.POINTER(BrunetOpts)]
     L.nmfc_brunet_default_opts.restype = None

@@ -50,7 +50,7 @@ class BrunetEngine:
             raise RuntimeError(f"nmfc_brunet_create failed: {_lib.last_error()}")
         self.h = h
         self.m, self.n = m, n
-        self.device = device   # HIP device ordinal (-1: the device current at creation)
+        self.device = self.L.nmfc_brunet_device(h)   # HIP ordinal resolved at creation (device -1: the current one)
 
     def close(self):
         if getattr(self, "h", None):

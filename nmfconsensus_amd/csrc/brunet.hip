@@ -828,6 +828,8 @@ nmfc_brunet* nmfc_brunet_create(int device, const double* A, int m, int n, int a
   return e;
 }
 
+int nmfc_brunet_device(const nmfc_brunet* e) { return e ? e->dev : -1; }
+
 void nmfc_brunet_destroy(nmfc_brunet* e) {
   if (!e) return;
   if (e->st) (void)hipStreamSynchronize(e->st);

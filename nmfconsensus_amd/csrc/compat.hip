@@ -108,27 +108,32 @@ void generateMatrix(const int* pm, const int* pn, const int* pk, init_t* pinit, 
 }
 
 // The engine behind nmf_mu is kept across calls with the same A (nmf.r calls nmf_mu once per restart on
-// one data matrix, nmf.r:41-45; R passes a fresh copy each time, so A is matched by shape and content).
-// Creating an engine uploads A and builds its two layouts, and its first run allocates the work buffers:
-// on the gct shape that is several times the whole MU loop.  NMFC_NMF_MU_CACHE=0 disables the cache.
+// one data matrix, nmf.r:41-45; R passes a fresh copy each time, so A is matched by shape and content: a
+// host copy of the cached A is compared byte for byte, one pass over A like the hash it replaces, and no
+// collision can reuse a stale A).  Creating an engine uploads A and builds its two layouts, and its first run
+// allocates the work buffers: on the gct shape that is several times the whole MU loop.  A failed run drops
+// the cached engine.  NMFC_NMF_MU_CACHE=0 disables the cache; nmfc_nmf_mu_release() frees it (HBM + host copy).
 namespace {
 std::mutex g_mu_lock;
 struct MuCache {
   nmfc_engine* e = nullptr;
   int m = 0, n = 0;
-  uint64_t hash = 0;   // no destructor: HIP may already be torn down when statics are destroyed at exit
+  std::vector<double>* a = nullptr;   // host copy of the cached A (no destructor: HIP may be torn down at exit)
 } g_mu;
 
-uint64_t hash_matrix(const double* a, size_t len) {   // FNV-1a over the bytes, 8 at a time
-  uint64_t h = 1469598103934665603ull;
-  for (size_t i = 0; i < len; ++i) {
-    uint64_t v;
-    memcpy(&v, a + i, 8);
-    h = (h ^ v) * 1099511628211ull;
-  }
-  return h;
+void mu_cache_drop() {   // g_mu_lock held
+  nmfc_engine_destroy(g_mu.e);
+  g_mu.e = nullptr;
+  g_mu.m = g_mu.n = 0;
+  delete g_mu.a;
+  g_mu.a = nullptr;
 }
 }  // namespace
+
+void nmfc_nmf_mu_release(void) {
+  std::lock_guard<std::mutex> lock(g_mu_lock);
+  mu_cache_drop();
+}
 
 // nmf_mu.c:84-315 on the GPU engine
 double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int* maxiter, const double* pTolX,
@@ -151,18 +156,17 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
   nmfc_engine* e = nullptr;
   if (cache) {
     lock.lock();
-    const uint64_t h = hash_matrix(a, (size_t)m * n);
-    if (g_mu.e && g_mu.m == m && g_mu.n == n && g_mu.hash == h) {
+    const size_t len = (size_t)m * n;
+    if (g_mu.e && g_mu.m == m && g_mu.n == n && memcmp(g_mu.a->data(), a, len * sizeof(double)) == 0) {
       e = g_mu.e;
     } else {
-      nmfc_engine_destroy(g_mu.e);
-      g_mu.e = nullptr;
+      mu_cache_drop();
       e = nmfc_engine_create(-1, a, m, n, 0);
       if (e) {
         g_mu.e = e;
         g_mu.m = m;
         g_mu.n = n;
-        g_mu.hash = h;
+        g_mu.a = new std::vector<double>(a, a + len);
       }
     }
   } else {
@@ -185,7 +189,10 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
   r.H = h0;
   const int ks[1] = {k};
   int rc = nmfc_engine_run(e, ks, 1, 1, &o, w0, h0, &r);
-  if (!cache) nmfc_engine_destroy(e);
+  if (!cache)
+    nmfc_engine_destroy(e);
+  else if (rc != 0)
+    mu_cache_drop();   // the engine may be in a broken state: never reuse it
   if (rc != 0) {
     fprintf(stderr, "Error in nmf_mu: %s\n", nmfc_last_error());
     return -1;
@@ -204,7 +211,8 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
 // calculatenorm.c:44-78 on device operands: d = a - w h and ||d||_F / sqrt(m n), one fused GPU pass +
 // a host sum of the per-block partials in block order (deterministic).  ms_out: device time of the pass.
 int nmfc_calculate_norm_dev(const double* da, const double* dw, const double* dh, double* dd, int m, int n, int k,
-                            double* norm_out, double* ms_out) {
+                            double* norm_out, double* ms_out, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
   if (!da || !dw || !dh || !dd || m <= 0 || n <= 0 || k <= 0 || !norm_out) return -1;
   // grid: gene blocks x column groups (>> 256 CUs of workgroups; fixed for (m, n): deterministic sum order)
   const int gx = (m + nmfc::NT - 1) / nmfc::NT;
@@ -214,24 +222,26 @@ int nmfc_calculate_norm_dev(const double* da, const double* dw, const double* dh
   double* dp = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
   int rc = -1;
-  if (hipMalloc(&dp, blocks * 8) != hipSuccess) goto done;
+  if (hipMallocAsync((void**)&dp, blocks * 8, st) != hipSuccess) goto done;   // stream-ordered: no device sync
   if (ms_out && (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess)) goto done;
-  if (ms_out) (void)hipEventRecord(ev[0], 0);
+  if (ms_out) (void)hipEventRecord(ev[0], st);
   switch (k) {   // rank known at compile time up to KMAX (the engine's range); the generic pass above it
 #define NMFC_NORM_K(KK)                                                                                        \
   case KK:                                                                                                    \
-    hipLaunchKernelGGL(nmfc::k_norm_partial_k<KK>, dim3(gx, gy), dim3(nmfc::NT), 0, 0, da, dw, dh, dd, m, n, dp); \
+    hipLaunchKernelGGL(nmfc::k_norm_partial_k<KK>, dim3(gx, gy), dim3(nmfc::NT), 0, st, da, dw, dh, dd, m, n, dp); \
     break;
     NMFC_NORM_K(1) NMFC_NORM_K(2) NMFC_NORM_K(3) NMFC_NORM_K(4) NMFC_NORM_K(5) NMFC_NORM_K(6) NMFC_NORM_K(7)
     NMFC_NORM_K(8) NMFC_NORM_K(9) NMFC_NORM_K(10) NMFC_NORM_K(11) NMFC_NORM_K(12) NMFC_NORM_K(13)
     NMFC_NORM_K(14) NMFC_NORM_K(15) NMFC_NORM_K(16)
 #undef NMFC_NORM_K
     default:
-      hipLaunchKernelGGL(nmfc::k_norm_partial, dim3(gx, gy), dim3(nmfc::NT), 0, 0, da, dw, dh, dd, m, n, k, dp);
+      hipLaunchKernelGGL(nmfc::k_norm_partial, dim3(gx, gy), dim3(nmfc::NT), 0, st, da, dw, dh, dd, m, n, k, dp);
   }
   if (hipGetLastError() != hipSuccess) goto done;
-  if (ms_out) (void)hipEventRecord(ev[1], 0);
-  if (hipMemcpy(part.data(), dp, blocks * 8, hipMemcpyDeviceToHost) != hipSuccess) goto done;
+  if (ms_out) (void)hipEventRecord(ev[1], st);
+  if (hipMemcpyAsync(part.data(), dp, blocks * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    goto done;
   {
     double ss = 0.0;
     for (int b = 0; b < blocks; ++b) ss += part[b];
@@ -246,14 +256,18 @@ int nmfc_calculate_norm_dev(const double* da, const double* dw, const double* dh
 done:
   for (hipEvent_t x : ev)
     if (x) (void)hipEventDestroy(x);
-  (void)hipFree(dp);
+  if (dp) {
+    (void)hipFreeAsync(dp, st);
+    (void)hipStreamSynchronize(st);
+  }
   return rc;
 }
 
 // calculatemaxchange.c:42-71 on device operands: max|mat0 - mat| / (sqrteps + max|mat0|); mat0 -= mat
 // (exact and order-free).
 int nmfc_calculate_maxchange_dev(const double* dm, double* dm0, int m, int n, double sqrteps, double* out,
-                                 double* ms_out) {
+                                 double* ms_out, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
   if (!dm || !dm0 || m <= 0 || n <= 0 || !out) return -1;
   const size_t len = (size_t)m * n;
   const int blocks = (int)std::min<size_t>((len + nmfc::NT - 1) / nmfc::NT, NORM_BLOCKS);
@@ -261,13 +275,15 @@ int nmfc_calculate_maxchange_dev(const double* dm, double* dm0, int m, int n, do
   double* dp = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
   int rc = -1;
-  if (hipMalloc(&dp, 2 * blocks * 8) != hipSuccess) goto done;
+  if (hipMallocAsync((void**)&dp, 2 * blocks * 8, st) != hipSuccess) goto done;
   if (ms_out && (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess)) goto done;
-  if (ms_out) (void)hipEventRecord(ev[0], 0);
-  hipLaunchKernelGGL(nmfc::k_maxchange_partial, dim3(blocks), dim3(nmfc::NT), 0, 0, dm, dm0, (long)len, dp);
+  if (ms_out) (void)hipEventRecord(ev[0], st);
+  hipLaunchKernelGGL(nmfc::k_maxchange_partial, dim3(blocks), dim3(nmfc::NT), 0, st, dm, dm0, (long)len, dp);
   if (hipGetLastError() != hipSuccess) goto done;
-  if (ms_out) (void)hipEventRecord(ev[1], 0);
-  if (hipMemcpy(part.data(), dp, 2 * blocks * 8, hipMemcpyDeviceToHost) != hipSuccess) goto done;
+  if (ms_out) (void)hipEventRecord(ev[1], st);
+  if (hipMemcpyAsync(part.data(), dp, 2 * blocks * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    goto done;
   {
     double mx0 = 0.0, mxd = 0.0;
     for (int b = 0; b < blocks; ++b) {
@@ -285,7 +301,10 @@ int nmfc_calculate_maxchange_dev(const double* dm, double* dm0, int m, int n, do
 done:
   for (hipEvent_t x : ev)
     if (x) (void)hipEventDestroy(x);
-  (void)hipFree(dp);
+  if (dp) {
+    (void)hipFreeAsync(dp, st);
+    (void)hipStreamSynchronize(st);
+  }
   return rc;
 }
 
@@ -298,7 +317,7 @@ double calculateNorm(double* a, double* w, double* h, double* d, int m, int n, i
   if (hipMemcpy(da, a, la * 8, hipMemcpyHostToDevice) || hipMemcpy(dw, w, lw * 8, hipMemcpyHostToDevice) ||
       hipMemcpy(dh, h, lh * 8, hipMemcpyHostToDevice))
     goto done;
-  if (nmfc_calculate_norm_dev(da, dw, dh, dd, m, n, k, &v, nullptr) != 0) goto done;
+  if (nmfc_calculate_norm_dev(da, dw, dh, dd, m, n, k, &v, nullptr, nullptr) != 0) goto done;
   if (hipMemcpy(d, dd, la * 8, hipMemcpyDeviceToHost)) goto done;
   result = v;
 done:
@@ -318,7 +337,7 @@ double calculateMaxchange(double* mat, double* mat0, int m, int n, const double 
   if (hipMalloc(&dm, len * 8) || hipMalloc(&dm0, len * 8)) goto done;
   if (hipMemcpy(dm, mat, len * 8, hipMemcpyHostToDevice) || hipMemcpy(dm0, mat0, len * 8, hipMemcpyHostToDevice))
     goto done;
-  if (nmfc_calculate_maxchange_dev(dm, dm0, m, n, sqrteps, &v, nullptr) != 0) goto done;
+  if (nmfc_calculate_maxchange_dev(dm, dm0, m, n, sqrteps, &v, nullptr, nullptr) != 0) goto done;
   if (hipMemcpy(mat0, dm0, len * 8, hipMemcpyDeviceToHost)) goto done;
   result = v;
 done:

@@ -591,6 +591,8 @@ void nmfc_engine_destroy(nmfc_engine* e) {
   delete e;
 }
 
+int nmfc_engine_device(const nmfc_engine* e) { return e ? e->dev : -1; }
+
 void nmfc_engine_set_timing(nmfc_engine* e, int enable) {
   if (!e) return;
   e->timing = enable > 0;
@@ -987,7 +989,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       checked = q;   // every poll is now complete
       HCHECK(hipMemcpy(si.data(), e->stop_iter.p, sizeof(int) * nj, hipMemcpyDeviceToHost));
       std::vector<RestartInfo> gone, live;
-      for (const RestartInfo& r : pk.ri) (si[r.rid] ? gone : live).push_back(r);
+      for (const RestartInfo& r : pk.ri) {
+        if (!si[r.rid])
+          live.push_back(r);
+        else if (!archived[r.rid])   // stopped restarts a skipped repack (below) left in pk are archived once
+          gone.push_back(r);
+      }
       if (archive(gone)) return -1;
       Packing np = pack(live);
       if (e->narrow_ok) {   // few live columns: block packing, so the narrow kernels run only the live blocks

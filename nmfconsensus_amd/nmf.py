@@ -101,7 +101,7 @@ class Engine:
             raise RuntimeError(f"nmfc_engine_create failed: {_lib.last_error()}")
         self.h = h
         self.m, self.n = m, n
-        self.device = device   # HIP device ordinal (-1: the device current at creation)
+        self.device = self.L.nmfc_engine_device(h)   # HIP ordinal resolved at creation (device -1: the current one)
 
     def close(self):
         if getattr(self, "h", None):
@@ -142,7 +142,9 @@ class Engine:
             label_rule: int = LABEL_ARGMAX, job_begin: int = 0, job_end: int = -1, W_init=None, H_init=None,
             want_factors: bool = False, want_counts: bool = True, counts_device_ptr: int | None = None,
             check_every: int = 4, min_init: int = 0, max_init: int = 1, verbose: bool = False,
-            TolX: float = 1e-4, TolFun: float = 1e-4, init_stream: int = INIT_LIBNMF) -> SweepResult:
+            TolX: float = 1e-4, TolFun: float = 1e-4, init_stream: int = INIT_LIBNMF, want_h: bool = False) -> SweepResult:
+        """One sweep of the (k, restart) job grid (or its shard [job_begin, job_end)).  want_factors: final W and
+        H of every job; want_h: final H only (the C3-sized checks: W of 1800 jobs is 1.7 GB of host memory)."""
         ks = [int(k) for k in ks]
         nk = len(ks)
         njobs_all = nk * R
@@ -179,8 +181,9 @@ class Engine:
         wflat = hflat = None
         if want_factors:
             wflat = np.zeros(sum(m * k for k in jk), dtype=np.float64)
-            hflat = np.zeros(sum(k * n for k in jk), dtype=np.float64)
             res.W = wflat.ctypes.data_as(_dp)
+        if want_factors or want_h:
+            hflat = np.zeros(sum(k * n for k in jk), dtype=np.float64)
             res.H = hflat.ctypes.data_as(_dp)
         wi = hi = None
         if W_init is not None or H_init is not None:
@@ -197,11 +200,13 @@ class Engine:
         if rc != 0:
             raise RuntimeError(f"nmfc_engine_run failed: {_lib.last_error()}")
         Ws = Hs = None
-        if want_factors:
-            Ws, Hs = [], []
+        if want_factors or want_h:
+            Ws = [] if want_factors else None
+            Hs = []
             wo = ho = 0
             for k in jk:
-                Ws.append(wflat[wo:wo + m * k].reshape((m, k), order="F"))
+                if want_factors:
+                    Ws.append(wflat[wo:wo + m * k].reshape((m, k), order="F"))
                 Hs.append(hflat[ho:ho + k * n].reshape((k, n), order="F"))
                 wo += m * k
                 ho += k * n

@@ -1,10 +1,14 @@
-"""Synthetic expression matrices for the benchmark configs, identical on every host.
+"""Synthetic expression matrices for the benchmark configs, bit-identical on every host.
 
 A = W* H* + E, non-negative fp64, m genes x n samples:
   W* ~ U(0,1) (m x 4); H* plants 4 equal sample groups (group g: H*[g, j] = 1 + U(0,1)/2, else U(0,1)/10);
-  E = 0.1 |N(0,1)| (Box-Muller); the result is scaled to mean 2.5 (the bundled gct's scale).
+  E = 0.1 |Z| with Z = sqrt(3) (U1 + U2 + U3 + U4 - 2) (Irwin-Hall: zero mean, unit variance, near-normal);
+  the result is scaled to mean 2.5 (the bundled gct's scale).
 Uniforms come from a counter-based splitmix64 (53-bit mantissas), so any shard can regenerate any
-entry; seed 20261015.
+entry; seed 20261015.  Only IEEE +, -, * and one correctly rounded sum (math.fsum) are used: no libm
+transcendentals and no BLAS, whose results depend on the host CPU's SIMD / kernel dispatch.  (Round 2's
+form, Box-Muller through numpy's log1p/cos plus a BLAS W* H*, gave different bits on the build container
+and on the GPU box; the C3 reference golden, tests/golden/golden_c3.npz, needs the same A on both.)
 """
 from __future__ import annotations
 
@@ -42,16 +46,25 @@ def uniforms(stream: int, count: int, seed: int = SEED) -> np.ndarray:
 
 
 def planted_matrix(m: int, n: int, kstar: int = 4, seed: int = SEED) -> np.ndarray:
-    """The synthetic A (m x n, Fortran order, fp64)."""
+    """The synthetic A (m x n, Fortran order, fp64), bit-identical on every host."""
+    import math
+
     Wst = uniforms(1, m * kstar, seed).reshape((m, kstar), order="F")
     grp = (np.arange(n) * kstar) // n
     u = uniforms(2, kstar * n, seed).reshape((kstar, n), order="F")
     Hst = np.where(np.arange(kstar)[:, None] == grp[None, :], 1.0 + 0.5 * u, 0.1 * u)
-    u1 = uniforms(3, m * n, seed)
-    u2 = uniforms(4, m * n, seed)
-    z = np.sqrt(-2.0 * np.log1p(-u1)) * np.cos(2.0 * np.pi * u2)   # Box-Muller
-    A = Wst @ Hst + 0.1 * np.abs(z).reshape((m, n), order="F")
-    A *= 2.5 / A.mean()
+    # W* H* as elementwise products summed in a fixed order (no BLAS, no FMA contraction)
+    A = np.multiply(Wst[:, :1], Hst[:1, :], order="F")
+    for q in range(1, kstar):
+        A += Wst[:, q:q + 1] * Hst[q:q + 1, :]
+    z = uniforms(3, m * n, seed)
+    for st in (4, 5, 6):
+        z += uniforms(st, m * n, seed)
+    z -= 2.0
+    z *= math.sqrt(3.0)
+    A += (0.1 * np.abs(z)).reshape((m, n), order="F")
+    del z
+    A *= 2.5 / (math.fsum(A.ravel(order="K")) / (m * n))
     return np.asfortranarray(A)
 
 

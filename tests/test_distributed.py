@@ -104,7 +104,7 @@ def _brunet_worker(rank, world, port, ret):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import torch.distributed as dist
-    from nmfconsensus_amd.distributed import run_sharded_restarts_with
+    from nmfconsensus_amd.distributed import run_sharded_with
     from pyoracle import Oracle
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -125,7 +125,7 @@ def _brunet_worker(rank, world, port, ret):
                 counts[ki] += (l[:, None] == l[None, :]).astype(np.int32)
         return counts
 
-    out = run_sharded_restarts_with(runner, ks, R, A.shape[1], rank=rank, world=world)
+    out = run_sharded_with(runner, ks, R, A.shape[1], rank=rank, world=world, unit="restart")
     if rank == 0:
         ret.put((out, runner(0, R)))
     dist.barrier()
@@ -147,3 +147,42 @@ def test_gloo_world2_brunet_restart_shards():
         assert p.exitcode == 0
     assert np.array_equal(out, ref)
     assert out[0].diagonal().tolist() == [5] * out.shape[1]
+
+
+class _FakeEngine:
+    """Engine stand-in for the host logic of RestartGroups (no GPU): counts = one per job at [k index, 0, 0]."""
+
+    def __init__(self, A, device, a_device_ptr=None, shape=None):
+        self.m, self.n = (shape if shape else np.asarray(A).shape)
+        self.device, self.h, self.calls = 0, 1, []
+
+    def close(self):
+        self.h = None
+
+    def run(self, ks, R, job_begin=0, job_end=-1, counts_device_ptr=None, **kw):
+        from nmfconsensus_amd.nmf import SweepResult
+        self.calls.append((job_begin, job_end))
+        nk, n = len(ks), self.n
+        jobs = np.arange(job_begin, job_end)
+        c = np.zeros((nk, n, n), dtype=np.int32)
+        np.add.at(c[:, 0, 0], jobs % nk, 1)
+        return SweepResult(ks=list(ks), R=R, n=n, counts=c, consensus=c / R, labels=np.tile(jobs[:, None], (1, n)),
+                           iters=jobs.astype(np.int32), stopped_early=np.ones(len(jobs), np.int32),
+                           seconds_total=1.0, job_begin=job_begin, job_end=job_end)
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 8])
+def test_restart_groups_split_and_merge(G):
+    """RestartGroups: contiguous sub-ranges covering the shard, results merged in job order, counts summed."""
+    from nmfconsensus_amd.distributed import RestartGroups
+    ks, R = [2, 3, 4], 7
+    grp = RestartGroups(np.zeros((10, 5)), device=0, groups=G, engine_cls=_FakeEngine)
+    res = grp.run(ks, R, job_begin=4, job_end=19)
+    calls = sorted(c for e in grp.engines for c in e.calls)
+    assert calls[0][0] == 4 and calls[-1][1] == 19
+    assert all(calls[i][1] == calls[i + 1][0] for i in range(len(calls) - 1))
+    assert np.array_equal(res.iters, np.arange(4, 19))
+    assert np.array_equal(res.counts[:, 0, 0], np.bincount(np.arange(4, 19) % 3, minlength=3))
+    grp.close()
+    with pytest.raises(ValueError):
+        RestartGroups(np.zeros((10, 5)), groups=9, engine_cls=_FakeEngine)

@@ -133,6 +133,26 @@ def test_nmf_mu_abi(golden):
     assert relfro(out["h0"], golden[f"fixed_k{k}_T10_H"]) < TOL
 
 
+def test_nmf_mu_cache_follows_content(golden, monkeypatch):
+    """The engine nmf_mu keeps across calls is reused only for the same A: A then A' (same shape, one entry
+    changed) then A again must each give what an uncached call gives (NMFC_NMF_MU_CACHE=0)."""
+    from nmfconsensus_amd import _lib, libnmf
+    A = golden["A_gct"]
+    A2 = A.copy(order="F")
+    A2[517, 23] += 0.25
+    W0, H0 = golden["init_k3_W"], golden["init_k3_H"]
+    cached = [libnmf.nmf_mu(X, W0, H0, 40) for X in (A, A2, A)]
+    monkeypatch.setenv("NMFC_NMF_MU_CACHE", "0")
+    fresh = [libnmf.nmf_mu(X, W0, H0, 40) for X in (A, A2)]
+    for c, f in zip(cached, fresh + fresh[:1]):
+        assert np.array_equal(c["w0"], f["w0"]) and np.array_equal(c["h0"], f["h0"])
+    assert not np.array_equal(cached[0]["h0"], cached[1]["h0"])
+    _lib.lib().nmfc_nmf_mu_release()
+    monkeypatch.delenv("NMFC_NMF_MU_CACHE")
+    again = libnmf.nmf_mu(A, W0, H0, 40)   # a fresh engine after the release
+    assert np.array_equal(again["h0"], fresh[0]["h0"])
+
+
 def test_nmf_mu_odd_iterations(golden, oracle):
     from nmfconsensus_amd import libnmf
     A = golden["A_gct"]
