@@ -117,10 +117,14 @@ std::vector<uint32_t> make_jump_table(int nchunks) {
 
 enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID_LABELS = 5, KID_COUNTS = 6, KID_SMALL = 7, KID_N = 8 };
 
-// Packing of a restart list into 64-column panels by first-fit decreasing (k descending, ties by rid;
-// a restart never straddles a panel), so the k = 10 / 6 / 5 panels' spare columns take small-k
-// restarts; panel count rounded up to a multiple of WTA_NPT (the large W^T A tile spans that many
-// panels).  Placement never changes a result bit (DESIGN.md "Determinism").
+// Packing of a restart list: first-fit decreasing (k descending, ties by rid) into 16-column blocks -- a restart
+// never straddles a block -- and blocks, in order, four to a 64-column panel; panel count rounded up to a
+// multiple of WTA_NPT (the large W^T A tile spans that many panels).  Against packing whole 64-column panels
+// (rounds 1-2) this costs ~1 % more columns (R = 200: 682 blocks for 675 blocks' worth of columns) and removes
+// every 16 x 16 block a restart shares with another: W^T A forms only the 4 diagonal Gram blocks per panel (not
+// 4 + 3 straddling ones), A h^T's E = W0 (h h^T) runs 4 K steps per 16-row block (not up to 12), and the narrow
+// tail kernels apply as soon as the live restarts fit their blocks.  Placement never changes a result bit
+// (DESIGN.md "Determinism").
 constexpr int WTA_NPT = 4;
 #ifndef NMFC_AHTW_NBUF
 #define NMFC_AHTW_NBUF 2
@@ -150,38 +154,35 @@ struct Packing {
 };
 
 Packing pack(const std::vector<RestartInfo>& in) {
-  Packing pk;
   std::vector<RestartInfo> srt(in);
   std::stable_sort(srt.begin(), srt.end(), [](const RestartInfo& a, const RestartInfo& b) {
     return a.k != b.k ? a.k > b.k : a.rid < b.rid;
   });
-  std::vector<int> fill;                          // per panel: columns used
-  std::vector<std::vector<RestartInfo>> members;  // per panel, in column order
-  int first_open = 0;                             // panels before it have < KMIN free columns
+  std::vector<int> fill;
+  std::vector<std::vector<RestartInfo>> members;
+  size_t first_open = 0;   // blocks before it have fewer than 2 free columns (k >= 2)
   for (RestartInfo r : srt) {
-    int p = first_open;
-    while (p < (int)fill.size() && fill[p] + r.k > PANEL) ++p;
-    if (p == (int)fill.size()) {
+    size_t b = first_open;
+    while (b < fill.size() && fill[b] + r.k > 16) ++b;
+    if (b == fill.size()) {
       fill.push_back(0);
       members.emplace_back();
     }
-    r.col0 = p * PANEL + fill[p];
-    fill[p] += r.k;
-    members[p].push_back(r);
-    while (first_open < (int)fill.size() && fill[first_open] > PANEL - 2) ++first_open;   // k >= 2
+    r.col0 = (int)b * 16 + fill[b];
+    fill[b] += r.k;
+    members[b].push_back(r);
+    while (first_open < fill.size() && fill[first_open] > 14) ++first_open;
   }
-  for (size_t p = 0; p < members.size(); ++p) {
+  const int nblocks = (int)members.size();
+  Packing pk;
+  pk.npanels = std::max(1, (nblocks + 3) / 4);
+  for (int p = 0; p < pk.npanels; ++p) {   // a panel = 4 consecutive blocks
     pk.prb.push_back((int)pk.ri.size());
-    for (const RestartInfo& r : members[p]) pk.ri.push_back(r);
+    for (int b = 4 * p; b < std::min(nblocks, 4 * p + 4); ++b)
+      for (const RestartInfo& r : members[b]) pk.ri.push_back(r);
     pk.pre.push_back((int)pk.ri.size());
   }
-  pk.npanels = (int)members.size();
-  if (pk.npanels == 0) {
-    pk.npanels = 1;
-    pk.prb = {0};
-    pk.pre = {0};
-  }
-  while (pk.npanels % WTA_NPT) {   // empty panels complete the last W^T A panel group
+  while (pk.npanels % WTA_NPT) {
     pk.prb.push_back((int)in.size());
     pk.pre.push_back((int)in.size());
     ++pk.npanels;
@@ -202,46 +203,6 @@ int narrow_blocks(const Packing& pk, int maxb) {
     nb = std::max(nb, (r.col0 + r.k + 15) / 16);
   }
   return nb <= maxb ? nb : 0;
-}
-
-// Block packing for the tail: restarts first-fit decreasing into 16-column blocks (a restart never straddles
-// a block), blocks in order from column 0, so a few live restarts occupy only a few narrow blocks.
-Packing pack_blocks(const std::vector<RestartInfo>& in, int& nblocks) {
-  std::vector<RestartInfo> srt(in);
-  std::stable_sort(srt.begin(), srt.end(), [](const RestartInfo& a, const RestartInfo& b) {
-    return a.k != b.k ? a.k > b.k : a.rid < b.rid;
-  });
-  std::vector<int> fill;
-  std::vector<std::vector<RestartInfo>> members;
-  for (RestartInfo r : srt) {
-    size_t b = 0;
-    while (b < fill.size() && fill[b] + r.k > 16) ++b;
-    if (b == fill.size()) {
-      fill.push_back(0);
-      members.emplace_back();
-    }
-    r.col0 = (int)b * 16 + fill[b];
-    fill[b] += r.k;
-    members[b].push_back(r);
-  }
-  nblocks = (int)members.size();
-  Packing pk;
-  pk.npanels = std::max(1, (nblocks + 3) / 4);
-  for (int p = 0; p < pk.npanels; ++p) {   // a panel = 4 consecutive blocks
-    pk.prb.push_back((int)pk.ri.size());
-    for (int b = 4 * p; b < std::min(nblocks, 4 * p + 4); ++b)
-      for (const RestartInfo& r : members[b]) pk.ri.push_back(r);
-    pk.pre.push_back((int)pk.ri.size());
-  }
-  while (pk.npanels % WTA_NPT) {
-    pk.prb.push_back((int)in.size());
-    pk.pre.push_back((int)in.size());
-    ++pk.npanels;
-  }
-  pk.ci.assign((size_t)pk.npanels * PANEL, ColInfo{0, 0, 0, 0});
-  for (const RestartInfo& r : pk.ri)
-    for (int a = 0; a < r.k; ++a) pk.ci[r.col0 + a] = ColInfo{r.sq_off, r.col0 % PANEL, r.k, r.rid};
-  return pk;
 }
 
 // Small-shape path (k_small_mu): restarts packed first-fit decreasing into 16-column blocks (a restart never
@@ -997,14 +958,6 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       }
       if (archive(gone)) return -1;
       Packing np = pack(live);
-      if (e->narrow_ok) {   // few live columns: block packing, so the narrow kernels run only the live blocks
-        int cols = 0, nb = 0;
-        for (const RestartInfo& r : live) cols += r.k;
-        if (cols <= 16 * e->narrow_maxb) {
-          Packing bp = pack_blocks(live, nb);
-          if (nb <= e->narrow_maxb && (long)bp.npanels * PANEL <= cap_cols) np = std::move(bp);
-        }
-      }
       if ((long)np.npanels * PANEL > cap_cols) {
         // first-fit decreasing is not monotone under removal: a (rare) larger packing would overrun
         // the buffers sized from the initial one, so keep the current placement until the next poll
