@@ -391,6 +391,25 @@ __device__ __forceinline__ bool panel_live(const int* __restrict__ prb, const in
 // GITEM (1-panel tiles): the Gram blocks run in 3 extra workgroups per (chunk, panel), their first three waves
 // each one candidate block as a 1-wave GTile<16, 16> (P, Q = the block's W rows; the rest of the wave set exits),
 // beside the W^T A workgroups instead of on their waves (bit-identical: see k_wta_narrow).
+// Gram candidate blocks of an NPT-panel tile, diagonal blocks first: cand < 4 NPT is the diagonal block
+// cand & 3 of panel cand >> 2; the rest are the 3 blocks per panel straddling two 16-column blocks (needed only
+// when a restart crosses a block boundary, which the engine's 16-column block packing never produces).
+// cand = t + ntj (w + NW x) then gives waves 0..3 of each sample-tile workgroup one diagonal block each when
+// ntj = 4, one Gram chain per SIMD (a wave w shares its SIMD with w + 4): 4 MFMAs on the SIMD's 128 per stage,
+// where the per-panel order (7 candidates per panel) put two chains on each of two SIMDs (+2.6 % W^T A, C3).
+template <int NPT>
+__device__ __forceinline__ void gram_cand(int cand, int& q, int& br, int& bc) {
+  if (cand < 4 * NPT) {
+    q = cand >> 2;
+    br = bc = cand & 3;
+  } else {
+    const int s = cand - 4 * NPT;
+    q = s / 3;
+    br = s % 3;
+    bc = br + 1;
+  }
+}
+
 template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1, bool ABLK = false, bool GRAM = true,
           bool GITEM = false>
 static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
@@ -457,8 +476,8 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
   }
   if (!any) return;
   if (threadIdx.x < NCAND) {
-    const int q = threadIdx.x / 7, x = threadIdx.x % 7;
-    const int br = x < 4 ? x : x - 4, bc = x < 4 ? x : x - 3;
+    int q, br, bc;
+    gram_cand<NPT>(threadIdx.x, q, br, bc);
     int nd = live[q];
     if (nd && br != bc) {
       const ColInfo c = ci[(long)(NPT * pg + q) * PANEL + 16 * bc];
@@ -489,8 +508,8 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
     my_ra[x] = 0;
     my_rb[x] = 0;
     if (cand < NCAND) {
-      const int q = cand / 7, xx = cand % 7;
-      const int br = xx < 4 ? xx : xx - 4, bc = xx < 4 ? xx : xx - 3;
+      int q, br, bc;
+      gram_cand<NPT>(cand, q, br, bc);
       my_need[x] = need[cand];
       my_ra[x] = 64 * q + 16 * br;
       my_rb[x] = 64 * q + 16 * bc;
