@@ -176,19 +176,31 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
     fprintf(stderr, "Error in nmf_mu: %s\n", nmfc_last_error());
     return -1;
   }
-  nmfc_sweep_opts o;
-  nmfc_default_opts(&o);
-  o.maxiter = *maxiter;
-  o.stop_rule = NMFC_STOP_REF_COMPAT;
-  o.check_every = 64;
   int32_t iters = 0, early = 0;
-  nmfc_result r = {};
-  r.iters = &iters;
-  r.stopped_early = &early;
-  r.W = w0;
-  r.H = h0;
-  const int ks[1] = {k};
-  int rc = nmfc_engine_run(e, ks, 1, 1, &o, w0, h0, &r);
+  // small shapes (the bundled gct): one team launch with a single upload / download (nmfc_engine_mu1);
+  // any other shape: the batched engine with a batch of one restart
+  const long m_pad = ((long)m + 127) / 128 * 128;
+  const char* team_env = getenv("NMFC_SMALL_KERNEL");
+  const char* small_env = getenv("NMFC_SMALL");
+  const bool team = m_pad <= 1024 && n <= 64 && !(team_env && strcmp(team_env, "single") == 0) &&
+                    !(small_env && atoi(small_env) == 0);
+  int rc;
+  if (team) {
+    rc = nmfc_engine_mu1(e, k, *maxiter, NMFC_STOP_REF_COMPAT, w0, h0, w0, h0, &iters, &early);
+  } else {
+    nmfc_sweep_opts o;
+    nmfc_default_opts(&o);
+    o.maxiter = *maxiter;
+    o.stop_rule = NMFC_STOP_REF_COMPAT;
+    o.check_every = 64;
+    nmfc_result r = {};
+    r.iters = &iters;
+    r.stopped_early = &early;
+    r.W = w0;
+    r.H = h0;
+    const int ks[1] = {k};
+    rc = nmfc_engine_run(e, ks, 1, 1, &o, w0, h0, &r);
+  }
   if (!cache)
     nmfc_engine_destroy(e);
   else if (rc != 0)

@@ -267,12 +267,24 @@ struct nmfc_engine {
   bool narrow_ok = true;                  // narrow end-of-sweep kernels allowed (env NMFC_NARROW=0 disables)
   int narrow_maxb = 3;                    // narrow form up to this many 16-column blocks (env NMFC_NARROW_MAXB)
   bool small_ok = true;                   // small-shape persistent kernel allowed (env NMFC_SMALL=0 disables)
+  int small_kernel = 0;                   // small shapes: 0 auto, 1 teams of workgroups (k_team_mu), 2 one workgroup
+                                          // per block (k_small_mu); env NMFC_SMALL_KERNEL=team|single
   DevBuf Acm, Arm, Ablk;   // Acm: small-shape kernel only; Ablk: K-blocked A for W^T A (see k_layout_a)
   // per-run buffers (grow-only)
   DevBuf W[2], H[2], Gpart, SWpart, SH, SHP, colact, Hfin, Wfin;
   DevBuf rinfo, stop_iter, stop_reason, unchanged, classes, n_stopped, Hstat, Wsnap;
   DevBuf prb, pre, colinfo, moves, finfo;
   DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp, smallblk;
+  DevBuf teamG, teamSW, teamFlag;   // k_team_mu: partial buffers, per-workgroup flags (+ the error word)
+  int team_occ = 0;                // resident k_team_mu workgroups per CU (occupancy query, once)
+  // nmfc_engine_mu1 (one restart, the nmf_mu drop-in): device and pinned staging [block | stop | W | H],
+  // its own partial buffers and flags (zeroed when allocated; tags continue from mu1_base, the iterations of
+  // earlier calls)
+  DevBuf mu1_dev, mu1_G, mu1_SW, mu1_flag;
+  char* mu1_host = nullptr;
+  size_t mu1_host_bytes = 0;
+  int mu1_base = -1;   // -1: the flags must be zeroed
+  int mu1_kprev = 16;  // staging rows [k, mu1_kprev) may hold a previous call's factors
   int jump_chunks = 0;
   int* h_stopped = nullptr;   // pinned, 2 slots
   // timing
@@ -356,7 +368,71 @@ hipError_t launch_small_g(nmfc_engine* e, int nblocks, int maxiter, int stop_rul
   return hipGetLastError();
 }
 
+// k_team_mu: teams of P = m_pad / 64 workgroups, as many teams as are resident at once (each team runs its
+// blocks one after another); partial buffers two per team, flags and the error word zeroed per launch, tags from 1.
+int team_count(nmfc_engine* e, int nblocks) {
+  const int P = (int)(e->m_pad / TEAM_ROWS);
+  if (!e->team_occ) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_team_mu<4>, 256, 0) != hipSuccess || occ < 1) occ = 1;
+    // teams must be co-resident (their workgroups wait for each other); the API's answer can overstate
+    // residency where SGPRs bind: at ~106 SGPRs at most 6 256-thread workgroups fit a CU (MI355X_MICROARCH.md,
+    // residency).  A team that still cannot meet ends with an error, it does not hang.
+    e->team_occ = std::min(occ, 6);
+  }
+  return std::max(1, std::min(nblocks, (int)((long)e->team_occ * e->ncu / P)));
+}
+
+int launch_team(nmfc_engine* e, int nblocks, int maxiter, int stop_rule) {
+  const int jb = (e->n + 15) / 16;
+  const int P = (int)(e->m_pad / TEAM_ROWS);
+  if (e->m_pad % TEAM_ROWS != 0 || P > TEAM_PMAX || jb < 1 || jb > 4) {
+    set_err("k_team_mu: m_pad %ld / n %d unsupported", e->m_pad, e->n);
+    return -1;
+  }
+  auto kern = jb == 1 ? k_team_mu<1> : jb == 2 ? k_team_mu<2> : jb == 3 ? k_team_mu<3> : k_team_mu<4>;
+  const int nteams = team_count(e, nblocks);
+  const long np = 16L * jb;
+  if (e->teamG.ensure(sizeof(double) * nteams * 2 * TEAM_PMAX * 16 * np) ||
+      e->teamSW.ensure(sizeof(double) * nteams * 2 * TEAM_PMAX * 256) ||
+      e->teamFlag.ensure(sizeof(unsigned) * (nteams * TEAM_PMAX + 16)))
+    return -1;
+  // flags zeroed per launch (tags start at 1); the error word sits behind them
+  HCHECK(hipMemsetAsync(e->teamFlag.p, 0, sizeof(unsigned) * (nteams * TEAM_PMAX + 16), e->st));
+  hipLaunchKernelGGL(kern, dim3(nteams * P), dim3(256), 0, e->st, e->smallblk.as<SmallBlock>(), nblocks, P,
+                     e->Acm.as<double>(), e->m_pad, e->n, e->n_pad, e->W[0].as<double>(), e->H[0].as<double>(), maxiter,
+                     stop_rule, e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->teamG.as<double>(),
+                     e->teamSW.as<double>(), e->teamFlag.as<unsigned>(), 0u,
+                     reinterpret_cast<int*>(e->teamFlag.as<unsigned>() + nteams * TEAM_PMAX), nullptr);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    set_err("k_team_mu launch: %s", hipGetErrorString(err));
+    return -1;
+  }
+  return 0;
+}
+
+// 1 if a k_team_mu launch reported a team that could not meet (bounded wait), after the stream is drained
+int team_failed(nmfc_engine* e, int nblocks) {
+  int v = 0;
+  const unsigned* w = e->teamFlag.as<unsigned>() + team_count(e, nblocks) * TEAM_PMAX;
+  if (hipMemcpy(&v, w, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  return v != 0;
+}
+
+// Team or single-workgroup kernel for a batch of nblocks blocks.  A team runs a block's iteration in ~7 us
+// against ~25 us for one workgroup (gct shape, tools/teambench.hip), but only team_count() teams are resident
+// (one 256-VGPR workgroup per CU) and a team runs its blocks one after another: teams win while each runs at
+// most 3 blocks (C1's 18 blocks: 2 per team), the single-workgroup kernel beyond (C2's 219 blocks run at
+// once, one per CU).
+bool use_team(nmfc_engine* e, int nblocks) {
+  if (e->small_kernel) return e->small_kernel == 1;
+  const int nt = team_count(e, nblocks);
+  return (nblocks + nt - 1) / nt <= 3;
+}
+
 int launch_small(nmfc_engine* e, int nblocks, int maxiter, int stop_rule) {
+  if (use_team(e, nblocks)) return launch_team(e, nblocks, maxiter, stop_rule);
   hipError_t err;
   const int jb = (e->n + 15) / 16;
   if (e->m_pad % 64 != 0 || e->n_pad != (jb <= 2 ? 32 : 64)) {   // k_small_mu's compile-time strides
@@ -482,6 +558,8 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_NARROW")) e->narrow_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_NARROW_MAXB")) e->narrow_maxb = std::min(8, std::max(1, atoi(s)));
   if (const char* s = getenv("NMFC_SMALL")) e->small_ok = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_SMALL_KERNEL"))
+    e->small_kernel = std::string(s) == "team" ? 1 : std::string(s) == "single" ? 2 : 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
     const std::string v(s);
     e->force_ahtw = v == "128" ? 0 : v == "64" ? 1 : -1;
@@ -545,9 +623,11 @@ void nmfc_engine_destroy(nmfc_engine* e) {
                     &e->stop_iter, &e->stop_reason, &e->unchanged, &e->classes, &e->n_stopped, &e->prb,
                     &e->pre,       &e->colinfo,   &e->moves,     &e->finfo,     &e->initjobs, &e->chunk_job,  &e->chunk_idx,
                     &e->jump,      &e->labels,    &e->slot,      &e->grp_begin, &e->grp_list,  &e->counts_tmp,
-                    &e->cons_tmp,  &e->Hstat,     &e->Wsnap,     &e->smallblk};
+                    &e->cons_tmp,  &e->Hstat,     &e->Wsnap,     &e->smallblk,  &e->teamG,    &e->teamSW,
+                    &e->teamFlag,  &e->mu1_dev,   &e->mu1_G,     &e->mu1_SW,    &e->mu1_flag};
   for (DevBuf* b : bufs) b->release();
   if (e->h_stopped) (void)hipHostFree(e->h_stopped);
+  if (e->mu1_host) (void)hipHostFree(e->mu1_host);
   if (e->st) (void)hipStreamDestroy(e->st);
   delete e;
 }
@@ -807,6 +887,10 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       if (launch_small(e, (int)sblocks.size(), opts.maxiter, opts.stop_rule)) return -1;
     }
     HCHECK(hipStreamSynchronize(st));
+    if (use_team(e, (int)sblocks.size()) && team_failed(e, (int)sblocks.size())) {
+      set_err("k_team_mu: a team of workgroups could not meet (not co-resident?)");
+      return -1;
+    }
     if (e->timing) drain_timing(e);
     it = opts.maxiter;   // every restart records its own stop iteration
   }
@@ -1144,6 +1228,92 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
             iters_enqueued, max_it, (double)tot_iters / nj, e->repacks,
             std::chrono::duration<double>(t_end - t_start).count());
   }
+  return 0;
+}
+
+// One restart of nmf_mu.c:84-315 with the fewest host round trips (the unchanged-R drop-in, nmf.r:41-45 calls
+// nmf_mu once per restart): the job as one 16-column block on one k_team_mu team; one upload of
+// [block | W0 | H0] from pinned staging, the launch, one download of [stop | W | H], one synchronisation.
+// The flags are not zeroed per call: tags continue after the previous call's (mu1_base).
+int nmfc_engine_mu1(nmfc_engine* e, int k, int maxiter, int stop_rule, const double* W0, const double* H0,
+                    double* W_out, double* H_out, int* iters, int* early) {
+  if (!e || !W0 || !H0 || !W_out || !H_out || maxiter < 0 || k < 1 || k > 16 || k > e->m || k > e->n ||
+      (stop_rule != NMFC_STOP_FIXED && stop_rule != NMFC_STOP_REF_COMPAT && stop_rule != NMFC_STOP_ARGMAX_STABLE)) {
+    set_err("nmfc_engine_mu1: bad arguments");
+    return -1;
+  }
+  const int m = e->m, n = e->n;
+  const int jb = (n + 15) / 16;
+  const int P = (int)(e->m_pad / TEAM_ROWS);
+  if (!e->small_ok || e->small_kernel == 2 || e->m_pad > 1024 || n > 64 || P > TEAM_PMAX) {
+    set_err("nmfc_engine_mu1: shape %d x %d is not a team shape (m_pad <= 1024, n <= 64)", m, n);
+    return -1;
+  }
+  HCHECK(hipSetDevice(e->dev));
+  const long mp = e->m_pad, np = e->n_pad;
+  const size_t off_stop = 256, off_w = 512, off_h = off_w + sizeof(double) * 16 * mp;
+  const size_t total = off_h + sizeof(double) * 16 * np;
+  if (e->mu1_host_bytes < total) {
+    if (e->mu1_host) (void)hipHostFree(e->mu1_host);
+    e->mu1_host = nullptr;
+    e->mu1_host_bytes = 0;
+    HCHECK(hipHostMalloc((void**)&e->mu1_host, total, 0));
+    memset(e->mu1_host, 0, total);
+    e->mu1_host_bytes = total;
+    e->mu1_kprev = 16;
+  }
+  if (e->mu1_dev.ensure(total) || e->mu1_G.ensure(sizeof(double) * 2 * TEAM_PMAX * 16 * 16 * jb) ||
+      e->mu1_SW.ensure(sizeof(double) * 2 * TEAM_PMAX * 256))
+    return -1;
+  if (!e->mu1_flag.p) e->mu1_base = -1;
+  if (e->mu1_flag.ensure(sizeof(unsigned) * TEAM_PMAX)) return -1;
+  if (e->mu1_base < 0 || e->mu1_base > (1 << 30)) {
+    HCHECK(hipMemsetAsync(e->mu1_flag.p, 0, sizeof(unsigned) * TEAM_PMAX, e->st));
+    e->mu1_base = 0;
+  }
+  char* hb = e->mu1_host;
+  SmallBlock blk{};
+  blk.col0 = 0;
+  blk.nr = 1;
+  blk.rid[0] = 0;
+  blk.k[0] = k;
+  blk.lc0[0] = 0;
+  memcpy(hb, &blk, sizeof(blk));
+  int* hstop = reinterpret_cast<int*>(hb + off_stop);
+  hstop[0] = hstop[1] = hstop[2] = 0;   // stop iteration, reason, team error word
+  double* hw = reinterpret_cast<double*>(hb + off_w);
+  double* hh = reinterpret_cast<double*>(hb + off_h);
+  for (int c = 0; c < k; ++c) memcpy(hw + c * mp, W0 + (long)c * m, sizeof(double) * m);   // W0 column c -> row c
+  for (int c = 0; c < k; ++c)
+    for (int j = 0; j < n; ++j) hh[c * np + j] = H0[c + (long)j * k];                     // k x n column-major
+  if (e->mu1_kprev > k) {   // rows a larger previous k left behind
+    memset(hw + k * mp, 0, sizeof(double) * (e->mu1_kprev - k) * mp);
+    memset(hh + k * np, 0, sizeof(double) * (e->mu1_kprev - k) * np);
+  }
+  e->mu1_kprev = k;
+  char* db = static_cast<char*>(e->mu1_dev.p);
+  HCHECK(hipMemcpyAsync(db, hb, total, hipMemcpyHostToDevice, e->st));
+  auto kern = jb == 1 ? k_team_mu<1> : jb == 2 ? k_team_mu<2> : jb == 3 ? k_team_mu<3> : k_team_mu<4>;
+  int* dstop = reinterpret_cast<int*>(db + off_stop);
+  hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, e->st, reinterpret_cast<const SmallBlock*>(db), 1, P, e->Acm.as<double>(),
+                     mp, n, np, reinterpret_cast<double*>(db + off_w), reinterpret_cast<double*>(db + off_h), maxiter,
+                     stop_rule, dstop, dstop + 1, e->mu1_G.as<double>(), e->mu1_SW.as<double>(),
+                     e->mu1_flag.as<unsigned>(), (unsigned)e->mu1_base, dstop + 2, nullptr);
+  HCHECK(hipGetLastError());
+  HCHECK(hipMemcpyAsync(hb + off_stop, db + off_stop, total - off_stop, hipMemcpyDeviceToHost, e->st));
+  HCHECK(hipStreamSynchronize(e->st));
+  if (hstop[2]) {
+    e->mu1_base = -1;
+    set_err("k_team_mu: the team could not meet (not co-resident?)");
+    return -1;
+  }
+  const int it = maxiter == 0 ? 0 : hstop[0];
+  e->mu1_base += it;   // one tag per iteration run
+  for (int c = 0; c < k; ++c) memcpy(W_out + (long)c * m, hw + c * mp, sizeof(double) * m);
+  for (int c = 0; c < k; ++c)
+    for (int j = 0; j < n; ++j) H_out[c + (long)j * k] = hh[c * np + j];
+  if (iters) *iters = it;
+  if (early) *early = hstop[1] == 1;
   return 0;
 }
 

@@ -1366,7 +1366,9 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // ---- stop bookkeeping (one thread), then every thread sees the new run flags ----
+    // ---- stop bookkeeping (one thread, after every wave has applied its W rule), then every thread sees the
+    // new run flags ----
+    __syncthreads();
     if (tid == 0) {
       for (int q = 0; q < nr; ++q) {
         if (!sm.run[q]) continue;
@@ -1400,6 +1402,390 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     const int c = x / NP, j = x % NP;
     if (j < n) H[(long)(blk.col0 + c) * n_pad + j] = sm.H[c][j];
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Team form of the small-shape loop (k_team_mu, round 3).  One workgroup per 16-column block (k_small_mu)
+// is bound by that CU's matrix pipe: ~512 MFMAs per wave per iteration, ~14 us, whatever k is.  Here a
+// block is run by a TEAM of P = m_pad / 64 workgroups; workgroup p owns genes [64p, 64p + 64) and keeps
+// its slice of A in registers for the whole launch, in both operand layouts:
+//   ag[s] = A[64p + 4s + (lane>>4)][16w + (lane&15)]   (B operand of G = W^T A, wave w = sample block w)
+//   af[t] = A[64p + 16w + (lane&15)][4t + (lane>>4)]   (B operand of F^T = h A^T, wave w = genes 16w..)
+// and its W rows as wg[s] = W[64p + 4s + (lane>>4)][c = lane&15] (A operand of G and W^T W) and in the
+// D layout wd[r] = W[64p + 16w + (lane&15)][c = (lane>>4) + 4r] (B operand of E^T = S W^T, the W rule).
+// Per iteration (nmf_mu.c:174-216) a workgroup forms its partial G and W^T W over its 64 genes (MFMA
+// chains in gene order, W^T W's four wave partials summed in wave order) and publishes them; every
+// workgroup then sums the P partials in workgroup order -- the same bits in every workgroup -- and repeats
+// the H update, h h^T and the stop rule redundantly, so only G and W^T W cross workgroups.  F^T = h A^T
+// (K = samples), E^T = (h h^T) W0^T and the W rule stay local.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the measured sc1 table): every
+// partial is stored `sc1` (write-through), every storing wave waits vmcnt(0), the workgroup barrier, then ONE
+// lane stores the workgroup's flag (`sc1`, the iteration's tag); a consumer polls all P flags at once (lane q
+// of wave 0 reads flag q, one coalesced `sc1` load per poll), meets at a workgroup barrier and reads the
+// partials with `sc1` loads only.  (The data-tagged granule form, R2, was measured slower here: 16 producers'
+// granules re-read per retry.)  Tags are tag_base + the team's iteration count (monotonic; a caller that
+// carries tag_base across launches need not zero the flags again), and the partials alternate between two
+// buffers by parity, so a workgroup one iteration ahead (flag = tag + 1) never overwrites what another still
+// reads.  The grid holds only as many teams as are resident at once (host-sized); a team runs its blocks one
+// after another.  Every wait is bounded: a team that cannot meet sets *err and ends (the host reports the
+// failure) instead of hanging.
+// Deterministic: every order is a function of (m_pad, n) only, so a job gives the same bits in any block.
+// ---------------------------------------------------------------------------------------------
+constexpr int TEAM_ROWS = 64;           // genes per workgroup of a team
+constexpr int TEAM_PMAX = 16;           // workgroups per team (m_pad <= 1024)
+constexpr long TEAM_SPIN_MAX = 1L << 22;   // re-reads before a team gives up (seconds; teams are co-resident)
+
+template <int NJ>
+struct TeamSmem {
+  double H[16][16 * NJ + 1];   // current H of the block (rows = columns c; padded: conflict-free row reads)
+  double G[16][16 * NJ];    // team sum of W^T A
+  double SWw[4][16][16];    // wave partials of W^T W
+  double SW[16][17];        // team sum of W^T W (zero across restarts)
+  double S[16][17];         // h h^T (zero across restarts)
+  double Wt[TEAM_ROWS][17]; // updated W rows, (gene, column), padded rows
+  int cls[SMALL_MAXR][64];  // classes (REF_COMPAT: windows i < k; ARGMAX_STABLE: samples)
+  int colr[16];             // restart slot of each column (-1: padding)
+  int run[SMALL_MAXR];
+  int unch[SMALL_MAXR];
+  int changed[SMALL_MAXR];
+  int nrun, ncol, abort;
+  SmallBlock blk;
+};
+
+typedef unsigned long long u64;
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<u64*>(p), (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load(reinterpret_cast<u64*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// sum of the P partials of one entry (slots `stride` doubles apart) in workgroup order; every slot is loaded
+// unconditionally (the buffers hold TEAM_PMAX slots) so the loads issue back to back with one wait
+__device__ __forceinline__ double team_sum(const double* g, long stride, int P) {
+  double v[TEAM_PMAX];
+#pragma unroll
+  for (int q = 0; q < TEAM_PMAX; ++q) v[q] = ld_sc1(g + q * stride);
+  double s = v[0];
+#pragma unroll
+  for (int q = 1; q < TEAM_PMAX; ++q)
+    if (q < P) s += v[q];
+  return s;
+}
+
+// SKIP != 0 only in tools/teambench.hip (phase cost breakdown): bit 0 no exchange (each workgroup uses its own
+// partials), 1 no G / W^T W MFMAs, 2 no h h^T, 3 no F / E MFMAs, 4 no stop check, 6 phase clock stamps.
+template <int NJ, int SKIP = 0>
+static __global__ __launch_bounds__(256) void k_team_mu(
+    const SmallBlock* __restrict__ blocks, int nblocks, int P, const double* __restrict__ Acm, long m_pad, int n,
+    long n_pad, double* __restrict__ W, double* __restrict__ H, int maxiter, int stop_rule,
+    int* __restrict__ stop_iter, int* __restrict__ stop_reason, double* __restrict__ Gx, double* __restrict__ SWx,
+    unsigned* __restrict__ flags, unsigned tag_base, int* __restrict__ err, long long* __restrict__ prof) {
+  constexpr int NP = 16 * NJ;
+  constexpr int NQ = NP / 4;
+  constexpr int HU = (16 * NP + 255) / 256;
+  __shared__ TeamSmem<NJ> sm;
+  const int team = blockIdx.x / P, p = blockIdx.x - team * P;
+  const int nteams = gridDim.x / P;
+  if (team >= nteams) return;   // grid not a multiple of P (host sizes it exactly)
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, lr = l >> 4, lc = l & 15;
+  const int sc = tid >> 4, sd = tid & 15;   // this thread's (c, d) entry of the 16 x 16 W^T W and h h^T
+  const long g0 = (long)TEAM_ROWS * p;
+  double* const gx = Gx + (long)team * 2 * TEAM_PMAX * 16 * NP;   // [team][buf][slot][16][NP]
+  double* const swx = SWx + (long)team * 2 * TEAM_PMAX * 256;      // [team][buf][slot][256]
+  unsigned* const fl = flags + (long)team * TEAM_PMAX;             // [team][slot]: one 64-byte line per team
+  // this workgroup's slice of A, resident for the whole launch (Acm is zero past m and n)
+  double ag[16], af[NQ];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) ag[s] = (w < NJ) ? Acm[(long)(16 * w + lc) * m_pad + g0 + 4 * s + lr] : 0.0;
+#pragma unroll
+  for (int t = 0; t < NQ; ++t) af[t] = Acm[(long)(4 * t + lr) * m_pad + g0 + 16 * w + lc];
+  if (tid == 0) sm.abort = 0;
+  unsigned epoch = 0;
+  long long prof_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, prof_t = 0;
+#define TEAM_STAMP(i)                                             \
+  if ((SKIP & 64) && p == 0 && tid == 0) {                        \
+    const long long t_ = (long long)__builtin_readcyclecounter(); \
+    if ((i) > 0) prof_acc[(i)] += t_ - prof_t;                    \
+    prof_t = t_;                                                  \
+  }
+  for (int b = team; b < nblocks; b += nteams) {
+    __syncthreads();   // the previous block's readers of sm are done
+    if (tid == 0) {
+      sm.blk = blocks[b];
+      int nc = 0;
+      for (int q = 0; q < sm.blk.nr; ++q) nc = max(nc, sm.blk.lc0[q] + sm.blk.k[q]);
+      sm.ncol = nc;
+      sm.nrun = sm.blk.nr;
+    }
+    if (tid < 16) sm.colr[tid] = -1;
+    __syncthreads();
+    const SmallBlock& blk = sm.blk;
+    const int nr = blk.nr, ncol = sm.ncol;
+    if (tid < nr)
+      for (int a = 0; a < blk.k[tid]; ++a) sm.colr[blk.lc0[tid] + a] = tid;
+    if (tid < SMALL_MAXR) {
+      sm.run[tid] = tid < nr;
+      sm.unch[tid] = 0;
+    }
+    for (int x = tid; x < SMALL_MAXR * 64; x += 256) (&sm.cls[0][0])[x] = 0;   // nmf_mu.c:132
+    for (int x = tid; x < 16 * NP; x += 256) {
+      const int c = x / NP, j = x % NP;
+      sm.H[c][j] = (j < n) ? H[(long)(blk.col0 + c) * n_pad + j] : 0.0;
+    }
+    double wg[16], wd[4];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) wg[s] = W[(long)(blk.col0 + lc) * m_pad + g0 + 4 * s + lr];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wd[r] = W[(long)(blk.col0 + lr + 4 * r) * m_pad + g0 + 16 * w + lc];
+    __syncthreads();
+    // per-thread constants of the block: the H entries (c, j) this thread updates (live columns, j < n) with
+    // their restart's columns [b0, b0 + kq), and whether W^T W entry (sc, sd) lies inside one restart
+    int he_c[HU], he_j[HU], he_q[HU], he_b0[HU], he_k[HU];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const int x = tid + 256 * u;
+      const int c = x / n, j = x - (x / n) * n;
+      const bool live = x < ncol * n;
+      const int q = live ? sm.colr[c] : -1;
+      he_c[u] = c;
+      he_j[u] = j;
+      he_q[u] = q;
+      he_b0[u] = q >= 0 ? blk.lc0[q] : 0;
+      he_k[u] = q >= 0 ? blk.k[q] : 0;
+    }
+    const int sq = sm.colr[sc];
+    const bool sw_live = sc < ncol && sd < ncol && sq >= 0 && sq == sm.colr[sd];
+    int wq[4];   // restart slot of this lane's W-rule columns lr + 4r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wq[r] = sm.colr[lr + 4 * r];
+    int runmask = (1 << nr) - 1;   // restarts still running (register copy of sm.run)
+    for (int iter = 1; iter <= maxiter; ++iter) {
+      TEAM_STAMP(0);
+      // ---- this workgroup's partials of G = W^T A (wave w: samples 16w..) and W^T W (wave w: genes 16w..) ----
+      d4 gacc = (d4){0.0, 0.0, 0.0, 0.0}, sacc = (d4){0.0, 0.0, 0.0, 0.0};
+      if (w < NJ && !(SKIP & 2)) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(wg[s], ag[s], gacc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < ((SKIP & 2) ? 0 : 4); ++s) {
+        const double v = wg[4 * w + s];
+        sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, sacc, 0, 0, 0);
+      }
+      ++epoch;
+      const unsigned tag = tag_base + epoch;
+      const int buf = epoch & 1;
+      double* const gxb = gx + (long)buf * TEAM_PMAX * 16 * NP;
+      double* const swb = swx + (long)buf * TEAM_PMAX * 256;
+      if (w < NJ) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (lr + 4 * r < ncol) {
+            if (SKIP & 1)
+              sm.G[lr + 4 * r][16 * w + lc] = gacc[r];
+            else
+              st_sc1(gxb + ((long)p * 16 + lr + 4 * r) * NP + 16 * w + lc, gacc[r]);
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sm.SWw[w][lr + 4 * r][lc] = sacc[r];
+      __syncthreads();
+      TEAM_STAMP(1);
+      const double sw_own = ((sm.SWw[0][sc][sd] + sm.SWw[1][sc][sd]) + sm.SWw[2][sc][sd]) + sm.SWw[3][sc][sd];
+      if (sw_live && !(SKIP & 1)) st_sc1(swb + (long)p * 256 + tid, sw_own);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+      __syncthreads();
+      if (tid == 0 && !(SKIP & 1)) __hip_atomic_store(fl + p, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      TEAM_STAMP(2);
+      // ---- wait for the P flags (lane q of wave 0 polls flag q), then the team sums in workgroup order ----
+      if (w == 0 && !(SKIP & 1)) {
+        bool mine = l >= P;
+        for (long spins = 0;; ++spins) {
+          if (!mine) mine = (int)(__hip_atomic_load(fl + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - tag) >= 0;
+          if (__all(mine)) break;
+          if (spins > TEAM_SPIN_MAX) {
+            if (l == 0) {
+              sm.abort = 1;
+              __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      TEAM_STAMP(3);
+      if (sm.abort) break;
+      if (!(SKIP & 1)) {
+        if (w < NJ) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = lr + 4 * r;
+            if (4 * r >= ncol) break;   // wave-uniform: no lane holds a live row from here on
+            const double v = team_sum(gxb + (long)c * NP + 16 * w + lc, 16L * NP, P);
+            if (c < ncol) sm.G[c][16 * w + lc] = v;
+          }
+        }
+        double v = 0.0;
+        if (sw_live) v = team_sum(swb + tid, 256, P);
+        sm.SW[sc][sd] = v;
+      } else {
+        sm.SW[sc][sd] = sw_live ? sw_own : 0.0;
+      }
+      if (tid < SMALL_MAXR) sm.changed[tid] = 0;
+      __syncthreads();
+      TEAM_STAMP(4);
+      if (sm.abort) break;
+      // ---- H update (nmf_mu.c:178, 184-191): d summed over the restart's columns in order ----
+      double hn[HU];
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        const int q = he_q[u];
+        hn[u] = 0.0;
+        if (q >= 0 && ((runmask >> q) & 1)) {
+          const int c = he_c[u], j = he_j[u], b0 = he_b0[u];
+          double dsum = 0.0;
+          for (int bb = 0; bb < he_k[u]; ++bb) dsum = fma(sm.SW[c][b0 + bb], sm.H[b0 + bb][j], dsum);
+          hn[u] = mu_rule(sm.H[c][j], sm.G[c][j], dsum);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < HU; ++u)
+        if (he_q[u] >= 0 && ((runmask >> he_q[u]) & 1)) sm.H[he_c[u]][he_j[u]] = hn[u];
+      __syncthreads();
+      TEAM_STAMP(5);
+      // ---- h h^T (wave 0, MFMA over the samples); the stop rule (nmf_mu.c:253-282) on waves 1-3 ----
+      const bool check = stop_rule != STOP_FIXED && iter > 1 && (iter % 2 == 0);
+      if (w == 0) {
+        double hv[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) hv[q] = sm.H[lc][4 * q + lr];
+        __builtin_amdgcn_sched_barrier(0);
+        d4 hh = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < ((SKIP & 4) ? 0 : NQ); ++q) hh = __builtin_amdgcn_mfma_f64_16x16x4f64(hv[q], hv[q], hh, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = lr + 4 * r;
+          const int qc = sm.colr[c];
+          sm.S[c][lc] = (qc >= 0 && qc == sm.colr[lc]) ? hh[r] : 0.0;
+        }
+      } else if (check && !(SKIP & 16)) {
+        if (stop_rule == STOP_REF_COMPAT) {
+          // window i of restart q reads the flat k x n column-major buffer at [i*n, i*n + k)
+          for (int x = tid - 64; x < nr * 16; x += 192) {
+            const int q = x >> 4, i = x & 15, kq = blk.k[q];
+            if (i >= kq || i >= n || !((runmask >> q) & 1)) continue;
+            int cl = 0;
+            double prev = 0.0;
+            for (int jj = 0; jj < kq; ++jj) {
+              const int f = i * n + jj, j = f / kq, a = f - j * kq;
+              const double v = sm.H[blk.lc0[q] + a][j];
+              if (jj > 0 && v > prev) cl = jj;
+              prev = v;
+            }
+            if (sm.cls[q][i] != cl) {
+              sm.cls[q][i] = cl;
+              sm.changed[q] = 1;
+            }
+          }
+        } else if (stop_rule == STOP_ARGMAX_STABLE) {
+          for (int x = tid - 64; x < nr * 64; x += 192) {
+            const int q = x >> 6, j = x & 63;
+            if (j >= n || !((runmask >> q) & 1)) continue;
+            int best = 0;
+            double bv = sm.H[blk.lc0[q]][j];
+            for (int a = 1; a < blk.k[q]; ++a) {
+              const double v = sm.H[blk.lc0[q] + a][j];
+              if (v > bv) {
+                bv = v;
+                best = a;
+              }
+            }
+            if (sm.cls[q][j] != best) {
+              sm.cls[q][j] = best;
+              sm.changed[q] = 1;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      TEAM_STAMP(6);
+      // ---- F^T = h A^T, E^T = (h h^T) W0^T, W rule (nmf_mu.c:198-216) on this wave's 16 genes ----
+      {
+        d4 f = (d4){0.0, 0.0, 0.0, 0.0}, e = (d4){0.0, 0.0, 0.0, 0.0};
+        double hv[NQ], sv[4];   // every LDS operand read before the MFMA chains (one LDS latency, not one per step)
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) hv[t] = sm.H[lc][4 * t + lr];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sv[q] = sm.S[lc][4 * q + lr];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < ((SKIP & 8) ? 0 : 4); ++q) e = __builtin_amdgcn_mfma_f64_16x16x4f64(sv[q], wd[q], e, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < ((SKIP & 8) ? 0 : NQ); ++t) f = __builtin_amdgcn_mfma_f64_16x16x4f64(hv[t], af[t], f, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (wq[r] >= 0 && ((runmask >> wq[r]) & 1)) wd[r] = mu_rule(wd[r], f[r], e[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sm.Wt[16 * w + lc][lr + 4 * r] = wd[r];
+      // ---- stop bookkeeping (wave 0, lane q = restart q; identical in every workgroup of the team) ----
+      if (w == 0) {
+        bool alive = false;
+        if (l < nr && ((runmask >> l) & 1)) {
+          int reason = 0;
+          if (check) {
+            if (!sm.changed[l]) {
+              const int u = sm.unch[l] + 1;
+              sm.unch[l] = u;
+              if (u >= 200) reason = 1;   // nmf_mu.c:269-271
+            } else {
+              sm.unch[l] = 0;
+            }
+          }
+          if (!reason && iter >= maxiter) reason = 2;
+          if (reason) {
+            sm.run[l] = 0;
+            if (p == 0) {
+              stop_iter[blk.rid[l]] = iter;
+              stop_reason[blk.rid[l]] = reason;
+            }
+          } else {
+            alive = true;
+          }
+        }
+        const u64 am = __ballot(alive);
+        if (l == 0) sm.nrun = (int)__popcll(am);
+      }
+      __syncthreads();   // every wave has applied its W rule under this iteration's run flags
+      TEAM_STAMP(7);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) wg[s] = sm.Wt[4 * s + lr][lc];
+      if (sm.nrun == 0) break;
+      int rm = 0;
+#pragma unroll
+      for (int q = 0; q < SMALL_MAXR; ++q) rm |= (q < nr && sm.run[q]) ? (1 << q) : 0;
+      runmask = rm;
+      TEAM_STAMP(8);
+    }
+    if (sm.abort) break;
+    // ---- final factors of the block back to the stacked layout ----
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (lr + 4 * r < ncol) W[(long)(blk.col0 + lr + 4 * r) * m_pad + g0 + 16 * w + lc] = wd[r];
+    if (p == 0)
+      for (int x = tid; x < 16 * NP; x += 256) {
+        const int c = x / NP, j = x % NP;
+        if (c < ncol && j < n) H[(long)(blk.col0 + c) * n_pad + j] = sm.H[c][j];
+      }
+  }
+  if ((SKIP & 64) && p == 0 && tid == 0 && prof)
+    for (int i = 0; i < 9; ++i) prof[i] = prof_acc[i];
+#undef TEAM_STAMP
 }
 
 // ---------------------------------------------------------------------------------------------

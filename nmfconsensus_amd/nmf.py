@@ -138,6 +138,23 @@ class Engine:
         b = self.L.nmfc_engine_kernel_bytes(self.h, kid, ctypes.byref(algo))
         return b, algo.value
 
+    def mu1(self, W0, H0, *, maxiter: int = 10000, stop_rule: int = STOP_REF_COMPAT):
+        """One restart from caller factors (W0 m x k, H0 k x n) on the small-shape team kernel: the per-call path
+        of the nmf_mu drop-in (nmfc_engine_mu1; m rounded up to 128 <= 1024, n <= 64).  Returns (W, H, iters,
+        stopped_early)."""
+        W = np.array(W0, dtype=np.float64, order="F", copy=True)
+        H = np.array(H0, dtype=np.float64, order="F", copy=True)
+        k = W.shape[1]
+        if W.shape != (self.m, k) or H.shape != (k, self.n):
+            raise ValueError(f"W0 {W.shape} / H0 {H.shape} do not match A {self.m}x{self.n}")
+        it, early = ctypes.c_int(0), ctypes.c_int(0)
+        dp = ctypes.POINTER(ctypes.c_double)
+        w, h = W.ctypes.data_as(dp), H.ctypes.data_as(dp)
+        if self.L.nmfc_engine_mu1(self.h, k, int(maxiter), int(stop_rule), w, h, w, h, ctypes.byref(it),
+                                  ctypes.byref(early)) != 0:
+            raise RuntimeError(f"nmfc_engine_mu1 failed: {_lib.last_error()}")
+        return W, H, it.value, bool(early.value)
+
     def run(self, ks, R: int, *, maxiter: int = 10000, seed: int = 123, stop_rule: int = STOP_REF_COMPAT,
             label_rule: int = LABEL_ARGMAX, job_begin: int = 0, job_end: int = -1, W_init=None, H_init=None,
             want_factors: bool = False, want_counts: bool = True, counts_device_ptr: int | None = None,

@@ -55,6 +55,42 @@ def test_fixed_iterations(gct_engine, golden, k, T):
 
 
 @pytest.mark.parametrize("k", [2, 3, 4, 5])
+def test_engine_mu1_vs_reference(gct_engine, golden, k):
+    """The nmf_mu per-call path (one restart on a k_team_mu team with one upload / launch / download,
+    nmfc_engine_mu1) against the reference-built golden: fixed counts within 1e-9, the REF_COMPAT exit exact.
+    Repeated calls also exercise the team counter carried across calls."""
+    W0, H0 = golden[f"init_k{k}_W"], golden[f"init_k{k}_H"]
+    for T in (2, 10, 200, 398):
+        W, H, it, early = gct_engine.mu1(W0, H0, maxiter=T, stop_rule=0)
+        assert it == T and not early
+        assert relfro(W, golden[f"fixed_k{k}_T{T}_W"]) < TOL and relfro(H, golden[f"fixed_k{k}_T{T}_H"]) < TOL, T
+    W, H, it, early = gct_engine.mu1(W0, H0, maxiter=10000, stop_rule=1)
+    assert it == int(golden[f"refc_k{k}_iter"]) and early
+    r = gct_engine.run([k], 1, maxiter=10000, seed=123, stop_rule=1, want_factors=True, want_counts=False)
+    # the same job through the batched entry runs the same team kernel alone in its block: the same bits
+    assert np.array_equal(r.W[0], W) and np.array_equal(r.H[0], H)
+
+
+@pytest.mark.parametrize("m,n,k", [(5, 4, 2), (300, 50, 16), (1024, 64, 7), (129, 17, 3)])
+def test_engine_mu1_shapes_vs_oracle(oracle, m, n, k):
+    """Team shapes at the edges: P = 2..16 workgroups, 1..4 sample blocks, k up to 16, ragged m and n."""
+    from nmfconsensus_amd.nmf import Engine
+    rng = np.random.default_rng(m * 1000 + n + k)
+    A = np.asfortranarray(rng.random((m, n)) + 0.05)
+    W0 = np.asfortranarray(rng.random((m, k)) + 0.01)
+    H0 = np.asfortranarray(rng.random((k, n)) + 0.01)
+    with Engine(A) as eng:
+        for T in (1, 2, 31):
+            W, H, it, _ = eng.mu1(W0, H0, maxiter=T, stop_rule=0)
+            Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, T, 0)
+            assert it == T
+            assert relfro(W, Wo) < TOL and relfro(H, Ho) < TOL, (m, n, k, T)
+        W, H, it, _ = eng.mu1(W0, H0, maxiter=3000, stop_rule=1)
+        _, _, ito = oracle.nmf_mu(A, W0, H0, 3000, 1)
+        assert it == ito
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 5])
 def test_ref_compat_exit(gct_engine, golden, k):
     r = gct_engine.run([k], 1, maxiter=10000, seed=123, stop_rule=1, want_factors=True, want_counts=False)
     assert r.iters[0] == int(golden[f"refc_k{k}_iter"])
@@ -320,14 +356,18 @@ def test_c1_runif_sweep_vs_reference(gct_engine, golden_c2, rule, key):
             assert relfro(r.H[j], g[f"c1r_H_k{k}"][q]) < TOL
 
 
-@pytest.mark.parametrize("rule,key", [(0, "argmax"), (1, "rorder")])
-def test_c2_sweep_vs_reference(golden_c2, rule, key):
+@pytest.mark.parametrize("rule,key,kernel", [(0, "argmax", "auto"), (1, "rorder", "auto"), (1, "rorder", "team")])
+def test_c2_sweep_vs_reference(golden_c2, rule, key, kernel, monkeypatch):
     """BASELINE configs[1] (C2): synthetic 1000 x 40, k = 2..8, R = 100 (700 jobs) in one sweep against the
-    reference's own nmf_mu run job by job: exits, labels, counts and consensus bit-exact; H within 1e-9."""
+    reference's own nmf_mu run job by job: exits, labels, counts and consensus bit-exact; H within 1e-9.
+    kernel "auto" runs the one-workgroup-per-block kernel at this batch size; "team" forces the team kernel,
+    whose teams then run ~14 blocks one after another (tag and buffer continuity across blocks)."""
     from nmfconsensus_amd.nmf import Engine
     g = golden_c2
     ks = [int(k) for k in g["c2_ks"]]
     R = int(g["c2_R"])
+    if kernel != "auto":
+        monkeypatch.setenv("NMFC_SMALL_KERNEL", kernel)
     with Engine(g["c2_A"]) as eng:
         r = eng.run(ks, R, maxiter=10000, seed=int(g["c2_seed"]), stop_rule=1, label_rule=rule, want_factors=True)
     assert np.array_equal(r.iters, g["c2_iters"])
