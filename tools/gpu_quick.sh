@@ -1,3 +1,5 @@
+#!/bin/bash
+# Quick check on one GPU: the -m gpu suite, smoke(), one default C3 bench line.  Usage: bash tools/gpu_quick.sh
 set -o pipefail
 OUT=gpurun_out/r03a
 mkdir -p $OUT

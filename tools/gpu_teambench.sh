@@ -1,3 +1,6 @@
+#!/bin/bash
+# tools/teambench (k_team_mu phase breakdown), the nmf_mu parity tests and the drop-in latency table.
+# Usage: bash tools/gpu_teambench.sh
 set -o pipefail
 OUT=gpurun_out/team2; mkdir -p $OUT
 timeout -k 10 120 ./tools/teambench 2000 > $OUT/teambench.txt 2>&1; rc=$?; cat $OUT/teambench.txt; [ $rc -eq 0 ] || exit 1
