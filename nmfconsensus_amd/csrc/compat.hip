@@ -177,12 +177,12 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
     return -1;
   }
   int32_t iters = 0, early = 0;
-  // small shapes (the bundled gct): one team launch with a single upload / download (nmfc_engine_mu1);
-  // any other shape: the batched engine with a batch of one restart
+  // small shapes (the bundled gct, expression sets up to 8192 genes x 64 samples): one team launch with a single
+  // upload / download (nmfc_engine_mu1); any other shape: the batched engine with a batch of one restart
   const long m_pad = ((long)m + 127) / 128 * 128;
   const char* team_env = getenv("NMFC_SMALL_KERNEL");
   const char* small_env = getenv("NMFC_SMALL");
-  const bool team = m_pad <= 1024 && n <= 64 && !(team_env && strcmp(team_env, "single") == 0) &&
+  const bool team = m_pad <= 8192 && n <= 64 && !(team_env && strcmp(team_env, "single") == 0) &&
                     !(small_env && atoi(small_env) == 0);
   int rc;
   if (team) {

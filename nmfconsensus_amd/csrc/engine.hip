@@ -267,8 +267,9 @@ struct nmfc_engine {
   bool narrow_ok = true;                  // narrow end-of-sweep kernels allowed (env NMFC_NARROW=0 disables)
   int narrow_maxb = 3;                    // narrow form up to this many 16-column blocks (env NMFC_NARROW_MAXB)
   bool small_ok = true;                   // small-shape persistent kernel allowed (env NMFC_SMALL=0 disables)
-  int small_kernel = 0;                   // small shapes: 0 auto, 1 teams of workgroups (k_team_mu), 2 one workgroup
-                                          // per block (k_small_mu); env NMFC_SMALL_KERNEL=team|single
+  int small_kernel = 0;                   // batched small shapes: 0/2 one workgroup per block (k_small_mu), 1 teams
+                                          // (k_team_mu); env NMFC_SMALL_KERNEL=team|single (single also keeps
+                                          // nmf_mu off the team path)
   DevBuf Acm, Arm, Ablk;   // Acm: small-shape kernel only; Ablk: K-blocked A for W^T A (see k_layout_a)
   // per-run buffers (grow-only)
   DevBuf W[2], H[2], Gpart, SWpart, SH, SHP, colact, Hfin, Wfin;
@@ -420,15 +421,15 @@ int team_failed(nmfc_engine* e, int nblocks) {
   return v != 0;
 }
 
-// Team or single-workgroup kernel for a batch of nblocks blocks.  A team runs a block's iteration in ~7 us
-// against ~25 us for one workgroup (gct shape, tools/teambench.hip), but only team_count() teams are resident
-// (one 256-VGPR workgroup per CU) and a team runs its blocks one after another: teams win while each runs at
-// most 3 blocks (C1's 18 blocks: 2 per team), the single-workgroup kernel beyond (C2's 219 blocks run at
-// once, one per CU).
+// Kernel for a batch of small-shape blocks: the one-workgroup k_small_mu, whatever the batch size, so a job
+// gives the same bits in any batch and on any number of GPUs (the consensus is then bit-identical at any GPU
+// count).  Teams (k_team_mu) serve the single-restart nmf_mu drop-in (nmfc_engine_mu1): a team runs a block's
+// iteration in ~7 us against ~25 us, but only team_count() teams are resident (one 256-VGPR workgroup per CU)
+// and a team runs its blocks one after another, so on C2's 219 blocks they are 2.5x slower
+// (profiles/r03/team/c2_kernels.txt).  NMFC_SMALL_KERNEL=team forces teams for batches too (tests).
 bool use_team(nmfc_engine* e, int nblocks) {
-  if (e->small_kernel) return e->small_kernel == 1;
-  const int nt = team_count(e, nblocks);
-  return (nblocks + nt - 1) / nt <= 3;
+  (void)nblocks;
+  return e->small_kernel == 1;
 }
 
 int launch_small(nmfc_engine* e, int nblocks, int maxiter, int stop_rule) {
@@ -581,7 +582,9 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   e->kchunk = (int)std::min<long>(kchunk, e->m_pad);
   e->nsplit = (int)((e->m_pad + e->kchunk - 1) / e->kchunk);
   // Acm (column-major, padded) feeds only the small-shape kernel; the general path's W^T A reads the K-blocked Ablk
-  const bool small_shape = e->m_pad <= 1024 && n <= 64;
+  // the column-major copy feeds the small-shape kernels: k_small_mu (m_pad <= 1024) and the team kernel
+  // behind nmfc_engine_mu1 (m_pad <= TEAM_ROWS * TEAM_PMAX = 8192)
+  const bool small_shape = e->m_pad <= (long)TEAM_ROWS * TEAM_PMAX && n <= 64;
   if ((small_shape && e->Acm.ensure(sizeof(double) * e->n_cols_pad * e->m_pad)) ||
       e->Ablk.ensure(sizeof(double) * e->n_cols_pad * e->m_pad) || e->Arm.ensure(sizeof(double) * e->m_pad * e->n_pad)) {
     nmfc_engine_destroy(e);
@@ -1245,8 +1248,9 @@ int nmfc_engine_mu1(nmfc_engine* e, int k, int maxiter, int stop_rule, const dou
   const int m = e->m, n = e->n;
   const int jb = (n + 15) / 16;
   const int P = (int)(e->m_pad / TEAM_ROWS);
-  if (!e->small_ok || e->small_kernel == 2 || e->m_pad > 1024 || n > 64 || P > TEAM_PMAX) {
-    set_err("nmfc_engine_mu1: shape %d x %d is not a team shape (m_pad <= 1024, n <= 64)", m, n);
+  if (!e->small_ok || e->small_kernel == 2 || n > 64 || P > TEAM_PMAX) {
+    set_err("nmfc_engine_mu1: shape %d x %d is not a team shape (m rounded up to 128 <= %d, n <= 64)", m, n,
+            TEAM_ROWS * TEAM_PMAX);
     return -1;
   }
   HCHECK(hipSetDevice(e->dev));

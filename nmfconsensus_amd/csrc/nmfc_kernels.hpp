@@ -1407,7 +1407,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
 // ---------------------------------------------------------------------------------------------
 // Team form of the small-shape loop (k_team_mu, round 3).  One workgroup per 16-column block (k_small_mu)
 // is bound by that CU's matrix pipe: ~512 MFMAs per wave per iteration, ~14 us, whatever k is.  Here a
-// block is run by a TEAM of P = m_pad / 64 workgroups; workgroup p owns genes [64p, 64p + 64) and keeps
+// block is run by a TEAM of P = m_pad / 64 workgroups (up to 128); workgroup p owns genes [64p, 64p + 64) and keeps
 // its slice of A in registers for the whole launch, in both operand layouts:
 //   ag[s] = A[64p + 4s + (lane>>4)][16w + (lane&15)]   (B operand of G = W^T A, wave w = sample block w)
 //   af[t] = A[64p + 16w + (lane&15)][4t + (lane>>4)]   (B operand of F^T = h A^T, wave w = genes 16w..)
@@ -1421,7 +1421,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
 // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the measured sc1 table): every
 // partial is stored `sc1` (write-through), every storing wave waits vmcnt(0), the workgroup barrier, then ONE
 // lane stores the workgroup's flag (`sc1`, the iteration's tag); a consumer polls all P flags at once (lane q
-// of wave 0 reads flag q, one coalesced `sc1` load per poll), meets at a workgroup barrier and reads the
+// (and q + 64) of wave 0 reads flag q, one coalesced `sc1` load per poll), meets at a workgroup barrier and reads the
 // partials with `sc1` loads only.  (The data-tagged granule form, R2, was measured slower here: 16 producers'
 // granules re-read per retry.)  Tags are tag_base + the team's iteration count (monotonic; a caller that
 // carries tag_base across launches need not zero the flags again), and the partials alternate between two
@@ -1432,7 +1432,8 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
 // Deterministic: every order is a function of (m_pad, n) only, so a job gives the same bits in any block.
 // ---------------------------------------------------------------------------------------------
 constexpr int TEAM_ROWS = 64;           // genes per workgroup of a team
-constexpr int TEAM_PMAX = 16;           // workgroups per team (m_pad <= 1024)
+constexpr int TEAM_PMAX = 128;          // workgroups per team (m_pad <= 8192)
+constexpr int TEAM_LB = 16;             // partials loaded per batch (in flight at once) when summing
 constexpr long TEAM_SPIN_MAX = 1L << 22;   // re-reads before a team gives up (seconds; teams are co-resident)
 
 template <int NJ>
@@ -1461,16 +1462,20 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
   return __longlong_as_double(
       (long long)__hip_atomic_load(reinterpret_cast<u64*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
-// sum of the P partials of one entry (slots `stride` doubles apart) in workgroup order; every slot is loaded
-// unconditionally (the buffers hold TEAM_PMAX slots) so the loads issue back to back with one wait
+// sum of the P partials of one entry (slots `stride` doubles apart) in workgroup order, in batches of TEAM_LB
+// loads issued back to back (every slot of a batch loaded unconditionally: the buffers hold TEAM_PMAX slots,
+// slots >= P are read but not summed), one wait per batch
 __device__ __forceinline__ double team_sum(const double* g, long stride, int P) {
-  double v[TEAM_PMAX];
+  double s = 0.0;
+  for (int q0 = 0; q0 < P; q0 += TEAM_LB) {
+    double v[TEAM_LB];
 #pragma unroll
-  for (int q = 0; q < TEAM_PMAX; ++q) v[q] = ld_sc1(g + q * stride);
-  double s = v[0];
+    for (int q = 0; q < TEAM_LB; ++q) v[q] = ld_sc1(g + (q0 + q) * stride);
+    if (q0 == 0) s = v[0];
 #pragma unroll
-  for (int q = 1; q < TEAM_PMAX; ++q)
-    if (q < P) s += v[q];
+    for (int q = 0; q < TEAM_LB; ++q)
+      if ((q0 > 0 || q > 0) && q0 + q < P) s += v[q];
+  }
   return s;
 }
 
@@ -1494,7 +1499,7 @@ static __global__ __launch_bounds__(256) void k_team_mu(
   const long g0 = (long)TEAM_ROWS * p;
   double* const gx = Gx + (long)team * 2 * TEAM_PMAX * 16 * NP;   // [team][buf][slot][16][NP]
   double* const swx = SWx + (long)team * 2 * TEAM_PMAX * 256;      // [team][buf][slot][256]
-  unsigned* const fl = flags + (long)team * TEAM_PMAX;             // [team][slot]: one 64-byte line per team
+  unsigned* const fl = flags + (long)team * TEAM_PMAX;             // [team][slot]
   // this workgroup's slice of A, resident for the whole launch (Acm is zero past m and n)
   double ag[16], af[NQ];
 #pragma unroll
@@ -1601,10 +1606,11 @@ static __global__ __launch_bounds__(256) void k_team_mu(
       TEAM_STAMP(2);
       // ---- wait for the P flags (lane q of wave 0 polls flag q), then the team sums in workgroup order ----
       if (w == 0 && !(SKIP & 1)) {
-        bool mine = l >= P;
+        bool mine = l >= P, mine2 = l + 64 >= P;   // lane l polls flags l and l + 64
         for (long spins = 0;; ++spins) {
           if (!mine) mine = (int)(__hip_atomic_load(fl + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - tag) >= 0;
-          if (__all(mine)) break;
+          if (!mine2) mine2 = (int)(__hip_atomic_load(fl + l + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - tag) >= 0;
+          if (__all(mine && mine2)) break;
           if (spins > TEAM_SPIN_MAX) {
             if (l == 0) {
               sm.abort = 1;

@@ -67,13 +67,15 @@ def test_engine_mu1_vs_reference(gct_engine, golden, k):
     W, H, it, early = gct_engine.mu1(W0, H0, maxiter=10000, stop_rule=1)
     assert it == int(golden[f"refc_k{k}_iter"]) and early
     r = gct_engine.run([k], 1, maxiter=10000, seed=123, stop_rule=1, want_factors=True, want_counts=False)
-    # the same job through the batched entry runs the same team kernel alone in its block: the same bits
-    assert np.array_equal(r.W[0], W) and np.array_equal(r.H[0], H)
+    # the batched entry runs the one-workgroup kernel (another fixed summation order): same exit, W/H to rounding
+    assert r.iters[0] == it and relfro(r.W[0], W) < 1e-11 and relfro(r.H[0], H) < 1e-11
 
 
-@pytest.mark.parametrize("m,n,k", [(5, 4, 2), (300, 50, 16), (1024, 64, 7), (129, 17, 3)])
+@pytest.mark.parametrize("m,n,k", [(5, 4, 2), (300, 50, 16), (1024, 64, 7), (129, 17, 3), (2000, 38, 3),
+                                   (5000, 38, 5), (8192, 64, 16), (8100, 33, 2)])
 def test_engine_mu1_shapes_vs_oracle(oracle, m, n, k):
-    """Team shapes at the edges: P = 2..16 workgroups, 1..4 sample blocks, k up to 16, ragged m and n."""
+    """Team shapes at the edges: P = 2..128 workgroups (partials summed in batches of 16), 1..4 sample blocks,
+    k up to 16, ragged m and n."""
     from nmfconsensus_amd.nmf import Engine
     rng = np.random.default_rng(m * 1000 + n + k)
     A = np.asfortranarray(rng.random((m, n)) + 0.05)
@@ -360,8 +362,8 @@ def test_c1_runif_sweep_vs_reference(gct_engine, golden_c2, rule, key):
 def test_c2_sweep_vs_reference(golden_c2, rule, key, kernel, monkeypatch):
     """BASELINE configs[1] (C2): synthetic 1000 x 40, k = 2..8, R = 100 (700 jobs) in one sweep against the
     reference's own nmf_mu run job by job: exits, labels, counts and consensus bit-exact; H within 1e-9.
-    kernel "auto" runs the one-workgroup-per-block kernel at this batch size; "team" forces the team kernel,
-    whose teams then run ~14 blocks one after another (tag and buffer continuity across blocks)."""
+    kernel "auto" runs the one-workgroup-per-block kernel (every batch does); "team" forces the team kernel, whose
+    teams then run ~14 blocks one after another (tag and buffer continuity across blocks)."""
     from nmfconsensus_amd.nmf import Engine
     g = golden_c2
     ks = [int(k) for k in g["c2_ks"]]
