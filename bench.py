@@ -159,6 +159,11 @@ def main():
                          "in turn on this GPU (as restart groups, the N > 1 policy); value = restarts / max shard time. "
                          "A replay of the real shards, not a scaling curve (C3/C4 MU engine, one process)")
     ap.add_argument("--dump-iters", default=None, help="write the last step's per-job iteration counts (.npy)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL, the measured path; gloo only to rehearse "
+                         "the N > 1 flow with several ranks on one GPU, together with --device)")
+    ap.add_argument("--device", type=int, default=None,
+                    help="HIP device of this rank (default LOCAL_RANK); rehearsal only")
     ap.add_argument("--cpu-kind", default="reference", choices=["reference", "port"],
                     help="reference: the reference's own nmf_mu (oracle/_ref, fails loudly when absent); port: the "
                          "oracle's C restatement")
@@ -169,12 +174,15 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) if args.device is None else args.device
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from nmfconsensus_amd.synthetic import CONFIGS, planted_matrix
     from nmfconsensus_amd.nmf import cophenetic_batch
@@ -376,7 +384,9 @@ def main():
                        "m": m, "n": n, "ks": ks, "restarts_per_k": R, "restarts_per_k_per_gpu": per_gpu,
                        "jobs": nk * R,
                        "parallelism": f"jobs sharded over {world} GPU(s) ({args.scaling} scaling), "
-                                      f"{G} restart group(s) per GPU, RCCL int32 all-reduce of counts",
+                                      f"{G} restart group(s) per GPU, "
+                                      + ("RCCL int32 all-reduce of counts" if args.dist_backend == "nccl"
+                                         else "gloo int32 all-reduce of counts (rehearsal, not a measurement)"),
                        "groups_per_gpu": G,
                        "mean_iterations": float(its.mean()), "max_iterations": int(its.max()),
                        "cophenetic_rho": {str(k): v for k, v in rho.items()}},
