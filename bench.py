@@ -132,7 +132,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--config", default="C3", choices=["C1", "C2", "C3", "C4", "C5"])
     ap.add_argument("--maxiter", type=int, default=10000)
     ap.add_argument("--stop-rule", default="ref_compat", choices=["fixed", "ref_compat", "argmax_stable"])
     ap.add_argument("--restarts", type=int, default=None, help="override R (restarts per k)")
@@ -193,6 +193,10 @@ def main():
         args.scaling = "weak" if args.config == "C4" else "strong"
     if args.config == "C5":
         return bench_brunet(args, rank, world, local, dev)
+    if args.config == "C1":
+        if world > 1:
+            raise SystemExit("C1 is the reference's one-process case (test_nmf.r)")
+        return bench_c1(args, dev)
     if args.simulate_world > 1:
         if world > 1:
             raise SystemExit("--simulate-world replays the shards in ONE process")
@@ -397,6 +401,96 @@ def main():
     groups.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def bench_c1(args, dev):
+    """BASELINE configs[0], the reference's own CPU-runnable case: test_nmf.r's
+    runNMFinJobs(read.gct("20+20x1000.gct"), k = 2:5, num.clusterings = 5, maxniter = 10000, seed = 123, njobs = 1)
+    -- 20 restarts (jobs in expand.grid order, job seed = seed + job_id - 1) on the bundled gct (its 1000 x 40
+    matrix from tests/golden/golden.npz, written there from the reference's file), REF_COMPAT stop rule.
+    A step = the batched sweep (one nmfc_engine_run: init, MU loops, labels, counts, consensus) -> `value`.
+    Beside it, timed once each: `dropin_flow` = the 20 restarts through the drop-in nmf_mu one call after another
+    (what nmf.r does unchanged on this library), and `cpu_baseline` = the same 20 calls of the REFERENCE's own
+    nmf_mu (oracle/_ref) on one core, as test_nmf.r's njobs = 1; both from the engine's init, whose W0/H0 equal
+    the reference's generateMatrix(ran) bit for bit (tests/test_gpu_parity.py), and their iteration counts
+    must agree with the sweep's."""
+    import numpy as np
+    import torch
+
+    from nmfconsensus_amd import _lib, libnmf
+    from nmfconsensus_amd.nmf import Engine
+
+    with np.load(os.path.join(ROOT, "tests", "golden", "golden.npz"), allow_pickle=False) as z:
+        A = np.asfortranarray(z["A_gct"])
+    m, n = A.shape
+    ks, R, seed = [2, 3, 4, 5], 5, 123
+    stop_rule = {"fixed": 0, "ref_compat": 1, "argmax_stable": 2}[args.stop_rule]
+    eng = Engine(A, device=dev.index)
+    for _ in range(args.warmup):
+        eng.run(ks, R, maxiter=args.maxiter, seed=seed, stop_rule=stop_rule)
+    eng.set_timing(not args.no_timing, 1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = eng.run(ks, R, maxiter=args.maxiter, seed=seed, stop_rule=stop_rule)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    value = len(ks) * R * args.steps / elapsed
+    roof = None
+    c, ms = eng.kernel_time(_lib.KID_SMALL)
+    if c:
+        fl = eng.kernel_flops(_lib.KID_SMALL)
+        ach = fl / (ms / c * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": "small_mu", "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                "note": "one persistent launch runs the whole sweep's MU loops (k_small_mu): algorithmic flop of all "
+                        "restart-iterations (4mnk + 4(m+n)k^2 each) / its HIP-event duration; latency-bound (the "
+                        "longest 16-column block sets the launch), SURVEY 8(d): C1/C2 fit in L2"}
+    init = eng.run(ks, R, maxiter=0, seed=seed, want_factors=True, want_counts=False)
+    eng.close()
+    its = np.asarray(res.iters)
+    jobs = [(np.asfortranarray(init.W[j]), np.asfortranarray(init.H[j])) for j in range(len(ks) * R)]
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    saved = os.dup(1)
+    os.dup2(devnull, 1)   # nmf_mu prints "Exiting nmf_mu after ..." per call (nmf_mu.c:296)
+    try:
+        libnmf.nmf_mu(A, *jobs[0], 10)   # engine for this A, code objects: not timed
+        t0 = time.perf_counter()
+        dropin_its = [libnmf.nmf_mu(A, W0, H0, args.maxiter)["maxiter"] for W0, H0 in jobs]
+        t_dropin = time.perf_counter() - t0
+        cpu = None
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            from pyoracle import RefLib
+            ref = RefLib()
+            t0 = time.perf_counter()
+            ref_its = [ref.nmf_mu(A, W0, H0, args.maxiter)[2] for W0, H0 in jobs]
+            t_ref = time.perf_counter() - t0
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+        os.close(devnull)
+    if not args.no_cpu_baseline:
+        cpu = {"value": len(jobs) / t_ref, "unit": "restarts/s", "cores": 1, "kind": "reference",
+               "sample": ("the whole C1 job: the reference's own nmf_mu (oracle/_ref, scipy OpenBLAS, 1 thread) on the "
+                          f"20 restarts one after another, as test_nmf.r's njobs = 1; {t_ref * 1e3:.1f} ms"),
+               "iterations_equal": bool(np.array_equal(np.asarray(ref_its), its)), "host": host_cpu()}
+    out = {
+        "metric": metric_name("C1", m, n, ks), "value": value, "unit": "restarts/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "the reference's bundled 20+20x1000.gct matrix (tests/golden/golden.npz); per-job generateMatrix(ran) init",
+        "config": {"workload": "C1: test_nmf.r -- runNMFinJobs(gct 1000x40, k=2:5, num.clusterings=5, maxniter=10000, "
+                               "seed=123), 20 restarts, stop rule " + args.stop_rule,
+                   "m": m, "n": n, "ks": ks, "restarts_per_k": R, "jobs": len(jobs),
+                   "mean_iterations": float(its.mean()), "max_iterations": int(its.max())},
+        "dropin_flow": {"value": len(jobs) / t_dropin, "unit": "restarts/s",
+                        "what": "the 20 restarts through the drop-in nmf_mu one call after another (nmf.r's .C path "
+                                f"unchanged, k_team_mu per call); {t_dropin * 1e3:.1f} ms",
+                        "iterations_equal": bool(np.array_equal(np.asarray(dropin_its), its))},
+        "roofline": roof, "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
 
 
 def bench_simulated_world(args, dev):
