@@ -50,10 +50,11 @@ typedef struct options_t {
  * runs on the GPU (HIP, gfx950).  Prints "Exiting nmf_mu after <iter>\n" like nmf_mu.c:296.
  * The stop rule is the reference's class-stability check (nmf_mu.c:253-282) in its defined
  * REF_COMPAT form.  Returns 0, or -1 on allocation / device failure (nmf_mu.c:138-151).
- * Rank limit: 2 <= k <= min(16, m, n).  The reference accepts any k; this engine keeps each
- * restart's k x k blocks in one 16-wide MFMA tile (KMAX, nmfconsensus_amd/csrc/nmfc_kernels.hpp), so
- * k > 16 (and k = 1, which nmf.r:107-108 never passes) prints "Error in nmf_mu: nmfc_engine_run: k=<k> unsupported ..." to stderr before any
- * device work, leaves w0/h0 untouched and returns -1.
+ * Ranks: 1 <= k <= min(m, n).  k = 2..16 runs on the MFMA engine (the team kernel for m <= 8192 genes, n <= 64
+ * samples, else the batched engine with a batch of one); any other k on the generic GPU path (nmfc_mu_generic,
+ * nmfconsensus_amd/csrc/generic.hip: plain fp64 products, one thread per output).  k outside 1..min(m, n) prints
+ * "Error in nmf_mu: k=<k> unsupported (need 1 <= k <= min(m, n))" to stderr before any device work, leaves
+ * w0/h0 untouched and returns -1.
  */
 double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int* maxiter,
               const double* pTolX, const double* pTolFun);

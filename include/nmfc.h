@@ -104,6 +104,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
  * ARGMAX_STABLE.  Returns 0, or -1 (nmfc_last_error) also for a shape outside the team range. */
 int nmfc_engine_mu1(nmfc_engine* e, int k, int maxiter, int stop_rule, const double* W0, const double* H0, double* W_out,
                     double* H_out, int* iters, int* early);
+/* One restart of nmf_mu for any rank 1 <= k <= min(m, n) on the generic GPU path (ranks the MFMA engine does not
+ * take, k > 16 or k = 1): the six products of nmf_mu.c:174-202 as plain fp64 contractions, the rules and the stop
+ * check as small kernels; A is kept on the device across calls with the same A (compared byte for byte).  Same
+ * argument meaning as nmfc_engine_mu1 (W m x k, H k x n column-major, updated in place). */
+int nmfc_mu_generic(const double* A, int m, int n, int k, int maxiter, int stop_rule, double* W, double* H, int* iters,
+                    int* early);
 int nmfc_sweep(const double* A, int m, int n, const int* ks, int nk, int R, const nmfc_sweep_opts* opts,
                nmfc_result* out);
 

@@ -145,10 +145,23 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
     printf("Exiting nmf_mu after %i\n", 1);
     return 0;
   }
-  if (k < 2 || k > nmfc::KMAX || k > m || k > n) {   // checked before any device work (libnmf_compat.h)
-    fprintf(stderr, "Error in nmf_mu: nmfc_engine_run: k=%d unsupported (need 2 <= k <= min(%d, m, n))\n", k,
-            nmfc::KMAX);
+  if (k < 1 || k > m || k > n) {   // checked before any device work (libnmf_compat.h)
+    fprintf(stderr, "Error in nmf_mu: k=%d unsupported (need 1 <= k <= min(m, n))\n", k);
     return -1;
+  }
+  if (k < 2 || k > nmfc::KMAX) {   // ranks outside the MFMA engine's 2..16: the generic GPU path
+    int iters = 0, early = 0;
+    if (nmfc_mu_generic(a, m, n, k, *maxiter, NMFC_STOP_REF_COMPAT, w0, h0, &iters, &early) != 0) {
+      fprintf(stderr, "Error in nmf_mu: %s\n", nmfc_last_error());
+      return -1;
+    }
+    int printed = iters;
+    if (early)
+      *maxiter = iters;
+    else
+      printed = iters + 1;
+    printf("Exiting nmf_mu after %i\n", printed);
+    return 0;
   }
   const char* cache_env = getenv("NMFC_NMF_MU_CACHE");
   const bool cache = !(cache_env && atoi(cache_env) == 0);

@@ -483,3 +483,39 @@ def test_full_c3_sweep_properties():
         assert np.array_equal(full.counts[i], cnt)
         assert np.array_equal(full.counts[i], full.counts[i].T) and np.all(np.diag(full.counts[i]) == R)
         assert np.array_equal(full.consensus[i], full.counts[i] / R)
+
+
+@pytest.mark.parametrize("m,n,k", [(300, 60, 20), (1000, 40, 17), (129, 33, 1), (500, 50, 24), (1000, 40, 5)])
+def test_generic_rank_path_vs_oracle(oracle, m, n, k):
+    """nmf_mu for ranks outside the MFMA engine's 2..16 (nmfc_mu_generic, csrc/generic.hip; also k = 5 as a
+    cross-check of the path itself): fixed counts within 1e-9, the REF_COMPAT exit exact."""
+    import ctypes
+    from nmfconsensus_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(7 * m + n + k)
+    A = np.asfortranarray(rng.random((m, n)) + 0.05)
+    W0 = np.asfortranarray(rng.random((m, k)) + 0.01)
+    H0 = np.asfortranarray(rng.random((k, n)) + 0.01)
+    dp = ctypes.POINTER(ctypes.c_double)
+    for T, rule in ((1, 0), (2, 0), (37, 0), (3000, 1)):
+        W, H = W0.copy(order="F"), H0.copy(order="F")
+        it, early = ctypes.c_int(0), ctypes.c_int(0)
+        rc = L.nmfc_mu_generic(A.ctypes.data_as(dp), m, n, k, T, rule, W.ctypes.data_as(dp), H.ctypes.data_as(dp),
+                               ctypes.byref(it), ctypes.byref(early))
+        assert rc == 0, _lib.last_error()
+        Wo, Ho, ito = oracle.nmf_mu(A, W0, H0, T, rule)
+        assert it.value == ito, (T, rule)
+        assert relfro(W, Wo) < TOL and relfro(H, Ho) < TOL, (m, n, k, T)
+
+
+def test_nmf_mu_abi_rank_above_16(golden):
+    """The drop-in takes ranks above 16 (the reference's nmf_mu takes any k): k = 20 on the gct through .C semantics."""
+    from nmfconsensus_amd import libnmf
+    from pyoracle import Oracle
+    A = golden["A_gct"]
+    rng = np.random.default_rng(20)
+    W0, H0 = rng.random((A.shape[0], 20)), rng.random((20, A.shape[1]))
+    out = libnmf.nmf_mu(A, W0, H0, 10000)
+    Wo, Ho, ito = Oracle().nmf_mu(A, W0, H0, 10000, 1)
+    assert out["ret"] == 0 and out["maxiter"] == ito
+    assert relfro(out["w0"], Wo) < TOL and relfro(out["h0"], Ho) < TOL
