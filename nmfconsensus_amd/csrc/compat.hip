@@ -197,10 +197,17 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
   const char* small_env = getenv("NMFC_SMALL");
   const bool team = m_pad <= 8192 && n <= 64 && !(team_env && strcmp(team_env, "single") == 0) &&
                     !(small_env && atoi(small_env) == 0);
-  int rc;
+  int rc = -1;
   if (team) {
-    rc = nmfc_engine_mu1(e, k, *maxiter, NMFC_STOP_REF_COMPAT, w0, h0, w0, h0, &iters, &early);
-  } else {
+    // w0/h0 are written only on success; a team that could not meet (its workgroups not all resident, e.g.
+    // many processes sharing the GPU, as BatchJobs njobs > 1 does) reports it instead of hanging, and the
+    // restart then runs on the batched engine, whose launches never wait for each other
+    // NMFC_TEAM_FAIL=1 (tests only) takes the fallback as if the team had failed
+    const char* tf = getenv("NMFC_TEAM_FAIL");
+    if (!(tf && atoi(tf) != 0))
+      rc = nmfc_engine_mu1(e, k, *maxiter, NMFC_STOP_REF_COMPAT, w0, h0, w0, h0, &iters, &early);
+  }
+  if (rc != 0) {
     nmfc_sweep_opts o;
     nmfc_default_opts(&o);
     o.maxiter = *maxiter;

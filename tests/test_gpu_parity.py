@@ -519,3 +519,16 @@ def test_nmf_mu_abi_rank_above_16(golden):
     Wo, Ho, ito = Oracle().nmf_mu(A, W0, H0, 10000, 1)
     assert out["ret"] == 0 and out["maxiter"] == ito
     assert relfro(out["w0"], Wo) < TOL and relfro(out["h0"], Ho) < TOL
+
+
+def test_nmf_mu_team_failure_falls_back(golden, monkeypatch):
+    """A drop-in call whose team cannot meet (e.g. many processes sharing the GPU) runs on the batched engine
+    instead: the same exit and W/H to rounding (NMFC_TEAM_FAIL simulates the failure)."""
+    from nmfconsensus_amd import libnmf
+    A, W0, H0 = golden["A_gct"], golden["init_k3_W"], golden["init_k3_H"]
+    team = libnmf.nmf_mu(A, W0, H0, 10000)
+    monkeypatch.setenv("NMFC_TEAM_FAIL", "1")
+    fb = libnmf.nmf_mu(A, W0, H0, 10000)
+    assert team["ret"] == 0 and fb["ret"] == 0
+    assert fb["maxiter"] == team["maxiter"] == int(golden["refc_k3_iter"])
+    assert relfro(fb["w0"], team["w0"]) < 1e-11 and relfro(fb["h0"], team["h0"]) < 1e-11
