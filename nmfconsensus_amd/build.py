@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib", "libnmf.so")
-SOURCES = ["engine.hip", "compat.hip", "brunet.hip", "generic.hip", "hclust.cpp"]
+SOURCES = ["engine.hip", "compat.hip", "brunet.hip", "generic.hip", "solo.hip", "hclust.cpp"]
 HEADERS = ["nmfc_kernels.hpp", "rmt.hpp", "../../include/nmfc.h", "../../include/libnmf_compat.h"]
 ARCH = os.environ.get("NMFC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

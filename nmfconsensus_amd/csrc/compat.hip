@@ -163,6 +163,22 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
     printf("Exiting nmf_mu after %i\n", printed);
     return 0;
   }
+  // small rank on a gct-sized matrix: one workgroup runs the whole restart (csrc/solo.hip); NMFC_SOLO=0 disables
+  const char* solo_env = getenv("NMFC_SOLO");
+  if (nmfc_mu_solo_fits(m, n, k) && !(solo_env && atoi(solo_env) == 0)) {
+    int iters = 0, early = 0;
+    if (nmfc_mu_solo(a, m, n, k, *maxiter, NMFC_STOP_REF_COMPAT, w0, h0, w0, h0, &iters, &early) != 0) {
+      fprintf(stderr, "Error in nmf_mu: %s\n", nmfc_last_error());
+      return -1;
+    }
+    int printed = iters;
+    if (early)
+      *maxiter = iters;
+    else
+      printed = iters + 1;
+    printf("Exiting nmf_mu after %i\n", printed);
+    return 0;
+  }
   const char* cache_env = getenv("NMFC_NMF_MU_CACHE");
   const bool cache = !(cache_env && atoi(cache_env) == 0);
   std::unique_lock<std::mutex> lock(g_mu_lock, std::defer_lock);

@@ -1,0 +1,421 @@
+// solo.hip -- nmf_mu for ONE restart of rank k = 2..4 on a small matrix (m <= 1024 genes, n <= 40 samples: the
+// bundled gct and data sets of its size), run by ONE workgroup (8 waves, one CU) through the whole MU loop and
+// the stop rule in one launch (nmf_mu.c:174-282).  The team kernel (k_team_mu) spreads such a restart over 16
+// CUs and pays three cross-XCD store -> load trips per iteration (~3.7 us of its 6.4 us at k = 2); one CU holds
+// the whole problem instead: A (320 KB at 1000 x 40) lives in the register file for the whole launch.
+//
+// Layout (4x4x4 f64 MFMA, 4 blocks b of 4 x 4 outputs, K = 4; lane 16 K + 4 b + i holds operand X_b[i][K] and
+// Y_b[K][i], result lane 16 i + 4 b + j holds D_b[i][j] -- profiles/r03/mfma_f64_4x4x4_probe.txt):
+//   lane l of wave w:  K = l >> 4, b = (l >> 2) & 3, j = l & 3;  gene(s) = 128 w + 16 s + 4 b + K, s < 8
+//   a_[s][cg] = A[gene(s)][4 cg + j]        (Y operand of G = W^T A: the reduction runs over genes)
+//   w_[s]     = W[gene(s)][j]               (X operand of G and of W^T W; j is the factor row a)
+// so G needs no data movement, with no padding of k beyond 4 (the 16x16x4 form pads k to 16).  F = A h^T
+// reduces over samples instead, which this layout spreads over the 4 lanes j of a quad and the 10 registers
+// cg: VALU fma chains over cg, then a quad butterfly (DPP); E = W0 (h h^T) and the W rule likewise per lane.
+// h h^T: three 4x4x4 MFMAs per wave over the 48 padded samples plus a 4-block butterfly, redundantly in
+// every wave (no barrier).  Per iteration: G / W^T W MFMAs -> LDS partials | barrier | wave and gene-block
+// sums in order | barrier | H update | barrier | stop check (wave 0) + h h^T, F, E, W rule (every wave).
+// Every reduction order is a function of (m, n, k) only: deterministic.  Stop rules and outputs as
+// nmfc_engine_mu1 (REF_COMPAT windows / ARGMAX_STABLE classes, stop iteration and reason).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/nmfc.h"
+#include "nmfc_kernels.hpp"
+
+void nmfc_set_error(const char* msg);
+
+namespace {
+
+using nmfc::mu_rule;
+
+constexpr int SOLO_W = 8;                        // waves (two per SIMD)
+constexpr int SOLO_S = 8;                        // 16-gene steps per wave
+constexpr int SOLO_MMAX = SOLO_W * SOLO_S * 16;  // 1024 genes
+constexpr int SOLO_NMAX = 40;                    // samples (10 column groups of 4 in registers)
+constexpr int SOLO_NCOLP = 48;                   // H columns in LDS (h h^T: 3 MFMA steps of 16 samples)
+
+template <int NCG>
+struct SoloSmem {
+  double Gp[SOLO_W][NCG + 1][64];   // wave partials of G (cg < NCG) and W^T W (NCG), MFMA D layout
+  double Hc[2][SOLO_NCOLP][4];      // H by (sample, row), rows padded to 4: zero past k and n
+  double Gs[4][4 * NCG];            // G = W^T A
+  double WW[4][4];                  // W^T W
+  int stop, reason;
+};
+
+// v from the lane given by the quad permutation CTRL (DPP, two 32-bit moves)
+template <int CTRL>
+__device__ __forceinline__ double qdpp(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u & 0xffffffffLL), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double qbcast(double v, int b) {   // lane b of the quad (b a compile-time constant)
+  switch (b) {
+    case 0: return qdpp<0x00>(v);
+    case 1: return qdpp<0x55>(v);
+    case 2: return qdpp<0xAA>(v);
+    default: return qdpp<0xFF>(v);
+  }
+}
+
+// SKIP != 0 only in tools/solobench.hip (phase costs): bit 0 no G / W^T W MFMAs, 1 no F / E / W rule, 2 no h h^T,
+// 3 no stop check, 4 no partial sums, 6 phase clock stamps of wave 0 into prof[1..7].
+template <int NCG, int KK, int SKIP = 0>
+__global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restrict__ A, int m, int n,
+                                                         double* __restrict__ W, double* __restrict__ H, int maxiter,
+                                                         int stop_rule, int* __restrict__ state,
+                                                         long long* __restrict__ prof = nullptr) {
+  static_assert(4 * (KK * (SOLO_NMAX - 8 * (KK - 2)) + KK * KK) <= 64 * SOLO_W, "one quad per summed entry");
+  constexpr int SB = KK == 2 ? 8 : 4;   // gene steps per F batch (larger: fewer H reads, more live registers)
+  __shared__ SoloSmem<NCG> sm;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, K = l >> 4, bq = (l >> 2) & 3, j = l & 3;
+  double a_[SOLO_S][NCG], w_[SOLO_S];
+#pragma unroll
+  for (int s = 0; s < SOLO_S; ++s) {
+    const int g = 128 * w + 16 * s + 4 * bq + K;
+#pragma unroll
+    for (int cg = 0; cg < NCG; ++cg) {
+      const int c = 4 * cg + j;
+      a_[s][cg] = (g < m && c < n) ? A[(long)c * m + g] : 0.0;
+    }
+    w_[s] = (g < m && j < KK) ? W[(long)j * m + g] : 0.0;
+  }
+  for (int x = tid; x < 2 * SOLO_NCOLP * 4; x += 64 * SOLO_W) (&sm.Hc[0][0][0])[x] = 0.0;
+  if (tid == 0) {
+    sm.stop = 0;
+    sm.reason = 0;
+  }
+  __syncthreads();
+  for (int x = tid; x < KK * n; x += 64 * SOLO_W) sm.Hc[0][x / KK][x % KK] = H[x];   // H is k x n column-major
+  __syncthreads();
+  long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = 0;
+#define SOLO_STAMP(i)                                             \
+  if ((SKIP & 64) && tid == 0) {                                  \
+    const long long t_ = (long long)__builtin_readcyclecounter(); \
+    if ((i) > 0) pacc[(i)] += t_ - pt;                            \
+    pt = t_;                                                      \
+  }
+  int hb = 0;
+  int cls = 0, unch = 0;   // wave 0: lane i's class (REF_COMPAT window i, ARGMAX_STABLE sample i), unchanged checks
+  for (int iter = 1; maxiter >= 1 && iter <= maxiter + 1; ++iter) {
+    SOLO_STAMP(0);
+    // ---- this wave's partials of G = W^T A and W^T W (MFMA chains in gene order) ----
+    {
+      double acc[NCG + 1];
+#pragma unroll
+      for (int cg = 0; cg <= NCG; ++cg) acc[cg] = 0.0;
+#pragma unroll
+      for (int s = 0; s < ((SKIP & 1) ? 0 : SOLO_S); ++s) {
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) acc[cg] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s], a_[s][cg], acc[cg], 0, 0, 0);
+        acc[NCG] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s], w_[s], acc[NCG], 0, 0, 0);
+      }
+#pragma unroll
+      for (int cg = 0; cg <= NCG; ++cg) sm.Gp[w][cg][l] = acc[cg];
+    }
+    SOLO_STAMP(1);
+    __syncthreads();
+    SOLO_STAMP(2);
+    if (sm.stop) break;   // decided at the previous iteration (its updates are done)
+    // ---- sums: G (k x n) and W^T W (k x k), four threads per entry (a quad): lane p sums waves 2p, 2p + 1
+    // (gene blocks b in order), then the quad butterfly ((p0 + p1) + (p2 + p3)) ----
+    {
+      const int o = tid >> 2, p = tid & 3;
+      if (!(SKIP & 16) && o < KK * n + KK * KK) {   // whole quads in or out (DPP below)
+        int a, c, cg, idx;
+        if (o < KK * n) {
+          a = o / n;
+          c = o - a * n;
+          cg = c >> 2;
+          idx = 16 * a + (c & 3);
+        } else {
+          a = (o - KK * n) / KK;
+          c = (o - KK * n) - a * KK;
+          cg = NCG;
+          idx = 16 * a + c;
+        }
+        const double* g0 = &sm.Gp[2 * p][cg][idx];
+        const double* g1 = &sm.Gp[2 * p + 1][cg][idx];
+        double v = ((g0[0] + g0[4]) + g0[8]) + g0[12];
+        v = (((v + g1[0]) + g1[4]) + g1[8]) + g1[12];
+        v = v + qdpp<0xB1>(v);
+        v = v + qdpp<0x4E>(v);
+        if (p == 0) {
+          if (o < KK * n)
+            sm.Gs[a][c] = v;
+          else
+            sm.WW[a][c] = v;
+        }
+      }
+    }
+    SOLO_STAMP(3);
+    __syncthreads();
+    // ---- H update (nmf_mu.c:178-191): d = (W^T W) H summed over the rows in order ----
+    const int nb = hb ^ 1;
+    for (int x = tid; x < KK * n; x += 64 * SOLO_W) {
+      const int c = x / KK, a = x - c * KK;
+      double d = 0.0;
+#pragma unroll
+      for (int b = 0; b < KK; ++b) d = fma(sm.WW[a][b], sm.Hc[hb][c][b], d);
+      sm.Hc[nb][c][a] = mu_rule(sm.Hc[hb][c][a], sm.Gs[a][c], d);
+    }
+    __syncthreads();
+    SOLO_STAMP(4);
+    hb = nb;
+    // ---- stop rule (nmf_mu.c:253-282), wave 0; read by every wave after the next iteration's first barrier ----
+    if (w == 0) {
+      const bool check = !(SKIP & 8) && stop_rule != nmfc::STOP_FIXED && iter > 1 && (iter % 2 == 0);
+      int reason = 0;
+      if (check) {
+        bool ch = false;
+        if (stop_rule == nmfc::STOP_REF_COMPAT) {
+          // window i reads the flat k x n column-major buffer at [i n, i n + k)
+          if (l < KK && l < n) {
+            int cl = 0;
+            double prev = 0.0;
+            for (int jj = 0; jj < KK; ++jj) {
+              const int f = l * n + jj, c = f / KK, a = f - c * KK;
+              const double v = sm.Hc[hb][c][a];
+              if (jj > 0 && v > prev) cl = jj;
+              prev = v;
+            }
+            ch = cl != cls;
+            cls = cl;
+          }
+        } else if (stop_rule == nmfc::STOP_ARGMAX_STABLE) {
+          if (l < n) {
+            int best = 0;
+            double bv = sm.Hc[hb][l][0];
+            for (int a = 1; a < KK; ++a) {
+              const double v = sm.Hc[hb][l][a];
+              if (v > bv) {
+                bv = v;
+                best = a;
+              }
+            }
+            ch = best != cls;
+            cls = best;
+          }
+        }
+        if (__ballot(ch) == 0) {
+          if (++unch >= 200) reason = 1;   // nmf_mu.c:269-271
+        } else {
+          unch = 0;
+        }
+      }
+      if (!reason && iter >= maxiter) reason = 2;
+      if (reason && l == 0) {
+        sm.stop = iter;
+        sm.reason = reason;
+      }
+    }
+    // ---- h h^T (4x4x4 MFMAs over the samples of block b, then the blocks in order), every wave ----
+    double hh = 0.0;
+#pragma unroll
+    for (int t = 0; t < ((SKIP & 4) ? 0 : SOLO_NCOLP / 16); ++t) {
+      const double x = sm.Hc[hb][16 * t + 4 * bq + K][j];
+      hh = __builtin_amdgcn_mfma_f64_4x4x4f64(x, x, hh, 0, 0, 0);
+    }
+    hh += __shfl_xor(hh, 4);
+    hh += __shfl_xor(hh, 8);
+    double hs[KK];   // (h h^T)[b][a], a = this lane's row (j; j & 1 when k = 2, two gene steps per pass)
+#pragma unroll
+    for (int b = 0; b < KK; ++b) hs[b] = __shfl(hh, 16 * b + (KK == 2 ? (j & 1) : j));
+    // ---- F = A h^T (this lane's samples 4 cg + j in order, then the quad), E = W0 (h h^T), W rule; genes in
+    // batches of SB steps (the H row block re-read from LDS per batch) to bound the live registers ----
+    const double* const hrow = &sm.Hc[hb][j][0];   // H[a][4 cg + j] at hrow[16 cg + a]
+    SOLO_STAMP(5);
+#pragma unroll
+    for (int s0 = 0; s0 < ((SKIP & 2) ? 0 : SOLO_S); s0 += SB) {
+      double P[SB][KK];
+#pragma unroll
+      for (int q = 0; q < SB; ++q)
+#pragma unroll
+        for (int a = 0; a < KK; ++a) P[q][a] = 0.0;
+      double h[KK], hn[KK];   // the next group's H loaded one step ahead
+      asm volatile("" ::: "memory");   // re-read H per batch: holding all of it would spill A
+#pragma unroll
+      for (int a = 0; a < KK; ++a) h[a] = hrow[a];
+#pragma unroll
+      for (int cg = 0; cg < NCG; ++cg) {
+        if (cg + 1 < NCG) {
+#pragma unroll
+          for (int a = 0; a < KK; ++a) hn[a] = hrow[16 * (cg + 1) + a];
+        }
+#pragma unroll
+        for (int q = 0; q < SB; ++q)
+#pragma unroll
+          for (int a = 0; a < KK; ++a) P[q][a] = fma(a_[s0 + q][cg], h[a], P[q][a]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int a = 0; a < KK; ++a) h[a] = hn[a];
+      }
+      if constexpr (KK == 2) {
+        // two gene steps per pass: lane j takes step s0 + q + (j >> 1), row a = j & 1 (lanes 2, 3 would idle)
+#pragma unroll
+        for (int q = 0; q < SB; q += 2) {
+          const int s = s0 + q, t = s + 1;
+          const bool hi = j >= 2;
+          // F: reduce-scatter of (s, 0), (s, 1), (t, 0), (t, 1) over the quad; lane j ends with entry j
+          const double k0 = hi ? P[q + 1][0] : P[q][0], k1 = hi ? P[q + 1][1] : P[q][1];
+          const double o0 = hi ? P[q][0] : P[q + 1][0], o1 = hi ? P[q][1] : P[q + 1][1];
+          const double q0 = k0 + qdpp<0x4E>(o0), q1 = k1 + qdpp<0x4E>(o1);   // partner j ^ 2
+          const double mine = (j & 1) ? q1 : q0, other = (j & 1) ? q0 : q1;
+          const double f = mine + qdpp<0xB1>(other);                         // partner j ^ 1
+          // this lane's W row: lanes 2, 3 take step t's values from lanes 0, 1
+          const double z = hi ? qdpp<0x44>(w_[t]) : w_[s];
+          double e = fma(qdpp<0xA0>(z), hs[0], 0.0);   // W0[g][0] from lane (j & 2)
+          e = fma(qdpp<0xF5>(z), hs[1], e);            // W0[g][1] from lane (j & 2) + 1
+          const double r = mu_rule(z, f, e);
+          const double rt = qdpp<0xEE>(r);             // step t's result back to lanes 0, 1
+          if (!hi) {
+            w_[s] = r;
+            w_[t] = rt;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+          const int s = s0 + q;
+          double f = 0.0;
+#pragma unroll
+          for (int a = 0; a < KK; ++a) {
+            double v = P[q][a];
+            v = v + qdpp<0xB1>(v);   // lanes j ^ 1
+            v = v + qdpp<0x4E>(v);   // lanes j ^ 2
+            f = (j == a) ? v : f;
+          }
+          double e = 0.0;
+#pragma unroll
+          for (int b = 0; b < KK; ++b) e = fma(qbcast(w_[s], b), hs[b], e);
+          if (j < KK) w_[s] = mu_rule(w_[s], f, e);
+        }
+      }
+    }
+    SOLO_STAMP(6);
+  }
+  if ((SKIP & 64) && tid == 0 && prof)
+    for (int i = 0; i < 8; ++i) prof[i] = pacc[i];
+#undef SOLO_STAMP
+  // ---- final factors and the stop state ----
+#pragma unroll
+  for (int s = 0; s < SOLO_S; ++s) {
+    const int g = 128 * w + 16 * s + 4 * bq + K;
+    if (g < m && j < KK) W[(long)j * m + g] = w_[s];
+  }
+  for (int x = tid; x < KK * n; x += 64 * SOLO_W) H[x] = sm.Hc[hb][x / KK][x % KK];
+  if (tid == 0) {
+    state[0] = sm.stop;
+    state[1] = sm.reason;
+  }
+}
+
+template <int NCG, int KK>
+hipError_t launch(const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule, int* st, hipStream_t s) {
+  hipLaunchKernelGGL((k_solo_mu<NCG, KK>), dim3(1), dim3(64 * SOLO_W), 0, s, A, m, n, W, H, maxiter, stop_rule, st);
+  return hipGetLastError();
+}
+
+struct SoloCache {   // device copy of the last A (compared byte for byte), work buffer, pinned staging
+  std::vector<double>* a = nullptr;   // no destructor: HIP may be torn down at exit
+  int m = 0, n = 0;
+  double* dA = nullptr;
+  double* dwork = nullptr;   // [state (2 ints, 16 B) | W m x k | H k x n]
+  double* pin = nullptr;     // pinned image of dwork
+  size_t cap = 0;            // doubles in dwork / pin
+  hipStream_t st = nullptr;
+};
+std::mutex g_lock;
+SoloCache g;
+
+int fail(const char* what, hipError_t e) {
+  char buf[256];
+  snprintf(buf, sizeof buf, "nmfc_mu_solo: %s: %s", what, hipGetErrorString(e));
+  nmfc_set_error(buf);
+  return -1;
+}
+
+}  // namespace
+
+#define SCHECK(x)                                \
+  do {                                           \
+    hipError_t e_ = (x);                         \
+    if (e_ != hipSuccess) return fail(#x, e_);   \
+  } while (0)
+
+// n <= 40 / 32 / 24 at k = 2 / 3 / 4: the kernels that keep A and their working set in registers without spilling
+extern "C" int nmfc_mu_solo_fits(int m, int n, int k) {
+  return m >= k && n >= k && k >= 2 && k <= 4 && m <= SOLO_MMAX && n <= SOLO_NMAX - 8 * (k - 2);
+}
+
+extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, int stop_rule, const double* W0,
+                            const double* H0, double* W, double* H, int* iters, int* early) {
+  if (!A || !W0 || !H0 || !W || !H || !nmfc_mu_solo_fits(m, n, k) || maxiter < 0 ||
+      (stop_rule != NMFC_STOP_FIXED && stop_rule != NMFC_STOP_REF_COMPAT && stop_rule != NMFC_STOP_ARGMAX_STABLE)) {
+    nmfc_set_error("nmfc_mu_solo: bad arguments (needs 2 <= k <= 4, k <= m <= 1024, k <= n <= 40)");
+    return -1;
+  }
+  std::lock_guard<std::mutex> lock(g_lock);
+  const size_t la = (size_t)m * n, lw = (size_t)m * k, lh = (size_t)k * n;
+  if (!g.st) SCHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
+  if (!(g.dA && g.m == m && g.n == n && memcmp(g.a->data(), A, la * sizeof(double)) == 0)) {
+    if (g.dA) (void)hipFree(g.dA);
+    g.dA = nullptr;
+    delete g.a;
+    g.a = new std::vector<double>(A, A + la);
+    g.m = m;
+    g.n = n;
+    SCHECK(hipMalloc(&g.dA, la * sizeof(double)));
+    SCHECK(hipMemcpyAsync(g.dA, A, la * sizeof(double), hipMemcpyHostToDevice, g.st));
+  }
+  const size_t need = 2 + lw + lh;
+  if (g.cap < need) {
+    if (g.dwork) (void)hipFree(g.dwork);
+    if (g.pin) (void)hipHostFree(g.pin);
+    g.dwork = g.pin = nullptr;
+    g.cap = 0;
+    SCHECK(hipMalloc(&g.dwork, need * sizeof(double)));
+    SCHECK(hipHostMalloc(&g.pin, need * sizeof(double), hipHostMallocDefault));
+    g.cap = need;
+  }
+  memcpy(g.pin + 2, W0, lw * sizeof(double));
+  memcpy(g.pin + 2 + lw, H0, lh * sizeof(double));
+  SCHECK(hipMemcpyAsync(g.dwork + 2, g.pin + 2, (lw + lh) * sizeof(double), hipMemcpyHostToDevice, g.st));
+  int* dstate = reinterpret_cast<int*>(g.dwork);
+  double* dW = g.dwork + 2;
+  double* dH = dW + lw;
+  // samples in column groups of 4: NCG = 4, 6, 8, 10 groups (n <= 16, 24, 32, 40) by k (nmfc_mu_solo_fits)
+  const int ncg = (n + 3) / 4;
+  const int gi = ncg <= 4 ? 0 : ncg <= 6 ? 1 : ncg <= 8 ? 2 : 3;
+  hipError_t le;
+  switch (k * 4 + gi) {
+    case 8: le = launch<4, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+    case 9: le = launch<6, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+    case 10: le = launch<8, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+    case 11: le = launch<10, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+    case 12: le = launch<4, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+    case 13: le = launch<6, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+    case 14: le = launch<8, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+    case 16: le = launch<4, 4>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+    case 17: le = launch<6, 4>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+    default: nmfc_set_error("nmfc_mu_solo: internal shape dispatch"); return -1;
+  }
+  SCHECK(le);
+  SCHECK(hipMemcpyAsync(g.pin, g.dwork, need * sizeof(double), hipMemcpyDeviceToHost, g.st));
+  SCHECK(hipStreamSynchronize(g.st));
+  int hstate[2];
+  memcpy(hstate, g.pin, sizeof hstate);
+  memcpy(W, g.pin + 2, lw * sizeof(double));
+  memcpy(H, g.pin + 2 + lw, lh * sizeof(double));
+  if (iters) *iters = maxiter == 0 ? 0 : hstate[0];
+  if (early) *early = hstate[1] == 1;
+  return 0;
+}

@@ -174,3 +174,20 @@ def test_cophenetic_batch_symmetric_fast_path():
     b = cophenetic_batch(Cs, nthreads=2, symmetric=True)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+def test_solo_path_shape_limits():
+    """The solo path's range (nmfc_mu_solo_fits) and its refusal of shapes outside it."""
+    import ctypes
+    from nmfconsensus_amd import _lib
+    L = _lib.lib()   # no device work: the range check comes first
+    assert L.nmfc_mu_solo_fits(1000, 40, 2) and L.nmfc_mu_solo_fits(1024, 32, 3) and L.nmfc_mu_solo_fits(1000, 24, 4)
+    for m, n, k in ((1000, 41, 2), (1025, 40, 2), (1000, 33, 3), (1000, 25, 4), (1000, 40, 5), (1000, 40, 1), (3, 2, 3)):
+        assert not L.nmfc_mu_solo_fits(m, n, k), (m, n, k)
+    dp = ctypes.POINTER(ctypes.c_double)
+    A = np.ones((1000, 41), order="F")
+    W, H = np.ones((1000, 2), order="F"), np.ones((2, 41), order="F")
+    it, early = ctypes.c_int(0), ctypes.c_int(0)
+    rc = L.nmfc_mu_solo(A.ctypes.data_as(dp), 1000, 41, 2, 10, 1, W.ctypes.data_as(dp), H.ctypes.data_as(dp),
+                        W.ctypes.data_as(dp), H.ctypes.data_as(dp), ctypes.byref(it), ctypes.byref(early))
+    assert rc == -1 and "bad arguments" in _lib.last_error()

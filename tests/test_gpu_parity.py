@@ -532,3 +532,30 @@ def test_nmf_mu_team_failure_falls_back(golden, monkeypatch):
     assert team["ret"] == 0 and fb["ret"] == 0
     assert fb["maxiter"] == team["maxiter"] == int(golden["refc_k3_iter"])
     assert relfro(fb["w0"], team["w0"]) < 1e-11 and relfro(fb["h0"], team["h0"]) < 1e-11
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 40, 2), (1024, 37, 2), (1000, 32, 3), (700, 24, 4), (640, 16, 2),
+                                   (37, 5, 4), (300, 29, 3), (129, 21, 4), (2, 9, 2)])
+def test_solo_path_vs_oracle(oracle, m, n, k):
+    """nmf_mu on one workgroup (nmfc_mu_solo, csrc/solo.hip: rank 2..4 on gct-sized matrices, A in one CU's
+    registers): fixed counts within 1e-9, the REF_COMPAT and ARGMAX_STABLE exits exact, ragged m and n."""
+    import ctypes
+    from nmfconsensus_amd import _lib
+    L = _lib.lib()
+    assert L.nmfc_mu_solo_fits(m, n, k) == 1
+    rng = np.random.default_rng(11 * m + n + k)
+    A = np.asfortranarray(rng.random((m, n)) + 0.05)
+    W0 = np.asfortranarray(rng.random((m, k)) + 0.01)
+    H0 = np.asfortranarray(rng.random((k, n)) + 0.01)
+    dp = ctypes.POINTER(ctypes.c_double)
+    for T, rule in ((1, 0), (2, 0), (37, 0), (3000, 1), (3000, 2)):
+        W, H = np.zeros_like(W0, order="F"), np.zeros_like(H0, order="F")
+        it, early = ctypes.c_int(0), ctypes.c_int(0)
+        rc = L.nmfc_mu_solo(A.ctypes.data_as(dp), m, n, k, T, rule, W0.ctypes.data_as(dp), H0.ctypes.data_as(dp),
+                            W.ctypes.data_as(dp), H.ctypes.data_as(dp), ctypes.byref(it), ctypes.byref(early))
+        assert rc == 0, _lib.last_error()
+        Wo, Ho, ito = oracle.nmf_mu(A, W0, H0, T, rule)
+        assert it.value == ito, (T, rule, it.value, ito)
+        assert bool(early.value) == (rule != 0 and ito < T), (T, rule)
+        assert relfro(W, Wo) < TOL and relfro(H, Ho) < TOL, (m, n, k, T, relfro(W, Wo), relfro(H, Ho))
+

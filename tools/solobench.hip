@@ -1,0 +1,83 @@
+// tools/solobench.hip -- phase cost breakdown of k_solo_mu (csrc/solo.hip: one workgroup runs a whole nmf_mu
+// restart) on the gct shape (1000 x 40): FIXED iterations, per-iteration time with phases removed, and the
+// phase clock stamps of wave 0.  Not part of the product.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/solobench.hip -o tools/solobench
+#include "../nmfconsensus_amd/csrc/solo.hip"
+
+void nmfc_set_error(const char* msg) { fprintf(stderr, "%s\n", msg); }
+
+#define CK(x)                                                                               \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess) {                                                                 \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                               \
+      exit(1);                                                                              \
+    }                                                                                       \
+  } while (0)
+
+template <int NCG, int KK>
+void bench(int m, int n, int T) {
+  std::vector<double> a((size_t)m * n), w((size_t)m * KK), h((size_t)KK * n);
+  for (size_t i = 0; i < a.size(); ++i) a[i] = 0.05 + ((i * 7919) % 1000) / 1000.0;
+  for (size_t i = 0; i < w.size(); ++i) w[i] = 0.01 + ((i * 104729) % 997) / 997.0;
+  for (size_t i = 0; i < h.size(); ++i) h[i] = 0.01 + ((i * 15485863) % 991) / 991.0;
+  double *dA, *dW, *dH;
+  int* st;
+  long long* prof;
+  CK(hipMalloc(&dA, a.size() * 8));
+  CK(hipMalloc(&dW, w.size() * 8));
+  CK(hipMalloc(&dH, h.size() * 8));
+  CK(hipMalloc(&st, 64));
+  CK(hipMalloc(&prof, 64));
+  CK(hipMemcpy(dA, a.data(), a.size() * 8, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  printf("k_solo_mu<%d, %d> on %d x %d, %d FIXED iterations\n", NCG, KK, m, n, T);
+  auto run = [&](auto kern, const char* name, bool stamps) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipMemcpy(dW, w.data(), w.size() * 8, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dH, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+      CK(hipEventRecord(e0));
+      hipLaunchKernelGGL(kern, dim3(1), dim3(64 * SOLO_W), 0, 0, dA, m, n, dW, dH, T, 0, st, prof);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best;
+    }
+    int hs[2];
+    CK(hipMemcpy(hs, st, 8, hipMemcpyDeviceToHost));
+    printf("  %-30s %8.3f ms  %7.2f us/iteration  (ran %d)\n", name, best, best * 1e3 / hs[0], hs[0]);
+    if (stamps) {
+      long long pc[8];
+      CK(hipMemcpy(pc, prof, sizeof pc, hipMemcpyDeviceToHost));
+      const char* nm[7] = {"", "G MFMA+store", "barrier 1", "sums", "H update+barriers", "stop+hhT", "F,E,W rule"};
+      long long tot = 0;
+      for (int i = 1; i < 7; ++i) tot += pc[i];
+      printf("    wave-0 cycles per iteration:");
+      for (int i = 1; i < 7; ++i) printf(" %s %lld |", nm[i], pc[i] / hs[0]);
+      printf(" sum %lld\n", tot / hs[0]);
+    }
+  };
+  run(k_solo_mu<NCG, KK, 0>, "full", false);
+  run(k_solo_mu<NCG, KK, 64>, "full, phase stamps", true);
+  run(k_solo_mu<NCG, KK, 1>, "no G MFMA", false);
+  run(k_solo_mu<NCG, KK, 2>, "no F/E/W", false);
+  run(k_solo_mu<NCG, KK, 4>, "no h h^T", false);
+  run(k_solo_mu<NCG, KK, 16>, "no partial sums", false);
+  run(k_solo_mu<NCG, KK, 3>, "no G, no F", false);
+  run(k_solo_mu<NCG, KK, 31>, "barriers + H update only", false);
+  CK(hipFree(dA));
+  CK(hipFree(dW));
+  CK(hipFree(dH));
+}
+
+int main(int argc, char** argv) {
+  const int T = argc > 1 ? atoi(argv[1]) : 2000;
+  bench<10, 2>(1000, 40, T);
+  bench<8, 3>(1000, 32, T);
+  bench<6, 4>(1000, 24, T);
+  return 0;
+}
