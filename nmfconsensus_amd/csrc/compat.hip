@@ -130,9 +130,14 @@ void mu_cache_drop() {   // g_mu_lock held
 }
 }  // namespace
 
+void nmfc_solo_release();   // solo.hip
+
 void nmfc_nmf_mu_release(void) {
-  std::lock_guard<std::mutex> lock(g_mu_lock);
-  mu_cache_drop();
+  {
+    std::lock_guard<std::mutex> lock(g_mu_lock);
+    mu_cache_drop();
+  }
+  nmfc_solo_release();
 }
 
 // nmf_mu.c:84-315 on the GPU engine

@@ -50,12 +50,20 @@ struct SoloSmem {
 };
 
 // v from the lane given by the quad permutation CTRL (DPP, two 32-bit moves)
+// (mov_dpp: no "old" operand to materialise; quad permutations never read outside the quad)
 template <int CTRL>
 __device__ __forceinline__ double qdpp(double v) {
   const long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u & 0xffffffffLL), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)(u & 0xffffffffLL), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xF, 0xF, true);
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+// nmfc::mu_rule without the early return (no divergent branch around the divide): the same operations in the
+// same order, so the same bits
+__device__ __forceinline__ double mu_rule_nb(double old, double num, double den) {
+  const double q = num / (den + nmfc::DIV_BY_ZERO_AVOIDANCE);
+  const double t = old * q;
+  return (old == 0.0 || num == 0.0 || t < 0.0) ? 0.0 : t;
 }
 __device__ __forceinline__ double qbcast(double v, int b) {   // lane b of the quad (b a compile-time constant)
   switch (b) {
@@ -68,13 +76,14 @@ __device__ __forceinline__ double qbcast(double v, int b) {   // lane b of the q
 
 // SKIP != 0 only in tools/solobench.hip (phase costs): bit 0 no G / W^T W MFMAs, 1 no F / E / W rule, 2 no h h^T,
 // 3 no stop check, 4 no partial sums, 6 phase clock stamps of wave 0 into prof[1..7].
-template <int NCG, int KK, int SKIP = 0>
+template <int NCG, int KK, int SKIP = 0, int SBO = 0>
 __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restrict__ A, int m, int n,
                                                          double* __restrict__ W, double* __restrict__ H, int maxiter,
                                                          int stop_rule, int* __restrict__ state,
                                                          long long* __restrict__ prof = nullptr) {
   static_assert(4 * (KK * (SOLO_NMAX - 8 * (KK - 2)) + KK * KK) <= 64 * SOLO_W, "one quad per summed entry");
-  constexpr int SB = KK == 2 ? 8 : 4;   // gene steps per F batch (larger: fewer H reads, more live registers)
+  // gene steps per F batch: larger means fewer H reads from LDS but more live registers (A holds most of them)
+  constexpr int SB = SBO ? SBO : KK == 2 ? 8 : 4;
   __shared__ SoloSmem<NCG> sm;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, K = l >> 4, bq = (l >> 2) & 3, j = l & 3;
   double a_[SOLO_S][NCG], w_[SOLO_S];
@@ -265,21 +274,23 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
           const int s = s0 + q, t = s + 1;
           const bool hi = j >= 2;
           // F: reduce-scatter of (s, 0), (s, 1), (t, 0), (t, 1) over the quad; lane j ends with entry j
+          // (every DPP read below runs with the whole quad active: no DPP under a lane-dependent branch)
           const double k0 = hi ? P[q + 1][0] : P[q][0], k1 = hi ? P[q + 1][1] : P[q][1];
           const double o0 = hi ? P[q][0] : P[q + 1][0], o1 = hi ? P[q][1] : P[q + 1][1];
-          const double q0 = k0 + qdpp<0x4E>(o0), q1 = k1 + qdpp<0x4E>(o1);   // partner j ^ 2
+          const double x0 = qdpp<0x4E>(o0), x1 = qdpp<0x4E>(o1);   // partner j ^ 2
+          const double q0 = k0 + x0, q1 = k1 + x1;
           const double mine = (j & 1) ? q1 : q0, other = (j & 1) ? q0 : q1;
-          const double f = mine + qdpp<0xB1>(other);                         // partner j ^ 1
+          const double y = qdpp<0xB1>(other);                       // partner j ^ 1
+          const double f = mine + y;
           // this lane's W row: lanes 2, 3 take step t's values from lanes 0, 1
-          const double z = hi ? qdpp<0x44>(w_[t]) : w_[s];
-          double e = fma(qdpp<0xA0>(z), hs[0], 0.0);   // W0[g][0] from lane (j & 2)
-          e = fma(qdpp<0xF5>(z), hs[1], e);            // W0[g][1] from lane (j & 2) + 1
-          const double r = mu_rule(z, f, e);
-          const double rt = qdpp<0xEE>(r);             // step t's result back to lanes 0, 1
-          if (!hi) {
-            w_[s] = r;
-            w_[t] = rt;
-          }
+          const double wt = qdpp<0x44>(w_[t]);
+          const double z = hi ? wt : w_[s];
+          const double z0 = qdpp<0xA0>(z), z1 = qdpp<0xF5>(z);     // W0[g][0], W0[g][1]: lanes (j & 2), (j & 2) + 1
+          const double e = fma(z1, hs[1], fma(z0, hs[0], 0.0));
+          const double r = mu_rule_nb(z, f, e);
+          const double rt = qdpp<0xEE>(r);                          // step t's result back to lanes 0, 1
+          w_[s] = hi ? w_[s] : r;
+          w_[t] = hi ? w_[t] : rt;
         }
       } else {
 #pragma unroll
@@ -296,7 +307,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
           double e = 0.0;
 #pragma unroll
           for (int b = 0; b < KK; ++b) e = fma(qbcast(w_[s], b), hs[b], e);
-          if (j < KK) w_[s] = mu_rule(w_[s], f, e);
+          if (j < KK) w_[s] = mu_rule_nb(w_[s], f, e);
         }
       }
     }
@@ -352,6 +363,19 @@ int fail(const char* what, hipError_t e) {
   } while (0)
 
 // n <= 40 / 32 / 24 at k = 2 / 3 / 4: the kernels that keep A and their working set in registers without spilling
+// nmfc_nmf_mu_release (compat.hip): the device copy of A, the work buffer and the pinned staging
+extern "C" void nmfc_solo_release() {
+  std::lock_guard<std::mutex> lock(g_lock);
+  if (g.dA) (void)hipFree(g.dA);
+  if (g.dwork) (void)hipFree(g.dwork);
+  if (g.pin) (void)hipHostFree(g.pin);
+  delete g.a;
+  g.a = nullptr;
+  g.dA = g.dwork = g.pin = nullptr;
+  g.cap = 0;
+  g.m = g.n = 0;
+}
+
 extern "C" int nmfc_mu_solo_fits(int m, int n, int k) {
   return m >= k && n >= k && k >= 2 && k <= 4 && m <= SOLO_MMAX && n <= SOLO_NMAX - 8 * (k - 2);
 }

@@ -23,9 +23,10 @@ def main():
     out = {"maxiter": 10000, "reps": reps, "shapes": {}}
     devnull = os.open(os.devnull, os.O_WRONLY)
     saved = os.dup(1)
-    for m, n in ((1000, 40), (2000, 38), (5000, 38), (8000, 60), (5000, 100)):
+    for m, n in ((1000, 40), (1000, 24), (600, 32), (2000, 38), (5000, 38), (8000, 60), (5000, 100)):
         A = planted_matrix(m, n)
-        libnmf.nmf_mu(A, *ref.generate_ran(1, m, n, 2), 10)   # engine for this A (cache), code objects
+        for k in (2, 5):   # the engine for this A (cache) and the solo path's copy, code objects
+            libnmf.nmf_mu(A, *ref.generate_ran(1, m, n, k), 10)
         res = {}
         for k in (2, 3, 5):
             W0, H0 = ref.generate_ran(123, m, n, k)

@@ -15,8 +15,8 @@ void nmfc_set_error(const char* msg) { fprintf(stderr, "%s\n", msg); }
     }                                                                                       \
   } while (0)
 
-template <int NCG, int KK>
-void bench(int m, int n, int T) {
+template <int NCG, int KK, int SBO = 0>
+void bench(int m, int n, int T, bool all = true) {
   std::vector<double> a((size_t)m * n), w((size_t)m * KK), h((size_t)KK * n);
   for (size_t i = 0; i < a.size(); ++i) a[i] = 0.05 + ((i * 7919) % 1000) / 1000.0;
   for (size_t i = 0; i < w.size(); ++i) w[i] = 0.01 + ((i * 104729) % 997) / 997.0;
@@ -33,7 +33,7 @@ void bench(int m, int n, int T) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  printf("k_solo_mu<%d, %d> on %d x %d, %d FIXED iterations\n", NCG, KK, m, n, T);
+  printf("k_solo_mu<%d, %d> (F batch %d) on %d x %d, %d FIXED iterations\n", NCG, KK, SBO, m, n, T);
   auto run = [&](auto kern, const char* name, bool stamps) {
     float best = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
@@ -61,7 +61,13 @@ void bench(int m, int n, int T) {
       printf(" sum %lld\n", tot / hs[0]);
     }
   };
-  run(k_solo_mu<NCG, KK, 0>, "full", false);
+  run(k_solo_mu<NCG, KK, 0, SBO>, "full", false);
+  if (!all) {
+    CK(hipFree(dA));
+    CK(hipFree(dW));
+    CK(hipFree(dH));
+    return;
+  }
   run(k_solo_mu<NCG, KK, 64>, "full, phase stamps", true);
   run(k_solo_mu<NCG, KK, 1>, "no G MFMA", false);
   run(k_solo_mu<NCG, KK, 2>, "no F/E/W", false);
@@ -79,5 +85,11 @@ int main(int argc, char** argv) {
   bench<10, 2>(1000, 40, T);
   bench<8, 3>(1000, 32, T);
   bench<6, 4>(1000, 24, T);
+  // F batch size (gene steps per H re-read) against register pressure, and the gct at k = 3, 4
+  bench<8, 3, 4>(1000, 32, T, false);
+  bench<6, 4, 1>(1000, 24, T, false);
+  bench<8, 4, 1>(1000, 32, T, false);
+  bench<10, 3, 1>(1000, 40, T, false);
+  bench<10, 4, 1>(1000, 40, T, false);
   return 0;
 }
