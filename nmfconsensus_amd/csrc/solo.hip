@@ -42,7 +42,9 @@ constexpr int SOLO_NCOLP = 48;                   // H columns in LDS (h h^T: 3 M
 
 template <int NCG>
 struct SoloSmem {
-  double Gp[SOLO_W][NCG + 1][64];   // wave partials of G (cg < NCG) and W^T W (NCG), MFMA D layout
+  // wave partials of G (cg < NCG) and W^T W (NCG) in the MFMA D layout, 64 doubles per (wave, cg); the wave
+  // stride is padded by 4 doubles so the four waves a summing quad reads fall in different LDS banks
+  double Gp[SOLO_W][(NCG + 1) * 64 + 4];
   double Hc[2][SOLO_NCOLP][4];      // H by (sample, row), rows padded to 4: zero past k and n
   double Gs[4][4 * NCG];            // G = W^T A
   double WW[4][4];                  // W^T W
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
         acc[NCG] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s], w_[s], acc[NCG], 0, 0, 0);
       }
 #pragma unroll
-      for (int cg = 0; cg <= NCG; ++cg) sm.Gp[w][cg][l] = acc[cg];
+      for (int cg = 0; cg <= NCG; ++cg) sm.Gp[w][cg * 64 + l] = acc[cg];
     }
     SOLO_STAMP(1);
     __syncthreads();
@@ -151,8 +153,8 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
           cg = NCG;
           idx = 16 * a + c;
         }
-        const double* g0 = &sm.Gp[2 * p][cg][idx];
-        const double* g1 = &sm.Gp[2 * p + 1][cg][idx];
+        const double* g0 = &sm.Gp[2 * p][cg * 64 + idx];
+        const double* g1 = &sm.Gp[2 * p + 1][cg * 64 + idx];
         double v = ((g0[0] + g0[4]) + g0[8]) + g0[12];
         v = (((v + g1[0]) + g1[4]) + g1[8]) + g1[12];
         v = v + qdpp<0xB1>(v);
@@ -233,8 +235,18 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
       const double x = sm.Hc[hb][16 * t + 4 * bq + K][j];
       hh = __builtin_amdgcn_mfma_f64_4x4x4f64(x, x, hh, 0, 0, 0);
     }
-    hh += __shfl_xor(hh, 4);
-    hh += __shfl_xor(hh, 8);
+    // blocks summed by DPP row rotations; only lanes with b = 0 are read below, where the order is
+    // (b0 + b1) + (b2 + b3)
+    {
+      const long long u = __double_as_longlong(hh);
+      const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)(u & 0xffffffffLL), 0x124, 0xF, 0xF, true);   // row_ror:4
+      const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0x124, 0xF, 0xF, true);
+      hh += __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+      const long long v = __double_as_longlong(hh);
+      const int lo2 = __builtin_amdgcn_mov_dpp((int)(unsigned)(v & 0xffffffffLL), 0x128, 0xF, 0xF, true);  // row_ror:8
+      const int hi2 = __builtin_amdgcn_mov_dpp((int)(v >> 32), 0x128, 0xF, 0xF, true);
+      hh += __longlong_as_double((long long)(((unsigned long long)(unsigned)hi2 << 32) | (unsigned)lo2));
+    }
     double hs[KK];   // (h h^T)[b][a], a = this lane's row (j; j & 1 when k = 2, two gene steps per pass)
 #pragma unroll
     for (int b = 0; b < KK; ++b) hs[b] = __shfl(hh, 16 * b + (KK == 2 ? (j & 1) : j));
@@ -245,10 +257,6 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
 #pragma unroll
     for (int s0 = 0; s0 < ((SKIP & 2) ? 0 : SOLO_S); s0 += SB) {
       double P[SB][KK];
-#pragma unroll
-      for (int q = 0; q < SB; ++q)
-#pragma unroll
-        for (int a = 0; a < KK; ++a) P[q][a] = 0.0;
       double h[KK], hn[KK];   // the next group's H loaded one step ahead
       asm volatile("" ::: "memory");   // re-read H per batch: holding all of it would spill A
 #pragma unroll
@@ -262,7 +270,8 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
 #pragma unroll
         for (int q = 0; q < SB; ++q)
 #pragma unroll
-          for (int a = 0; a < KK; ++a) P[q][a] = fma(a_[s0 + q][cg], h[a], P[q][a]);
+          for (int a = 0; a < KK; ++a)   // the chain's first term is a product (fma onto +0 but for the zero's sign)
+            P[q][a] = cg == 0 ? a_[s0 + q][0] * h[a] : fma(a_[s0 + q][cg], h[a], P[q][a]);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int a = 0; a < KK; ++a) h[a] = hn[a];

@@ -191,6 +191,25 @@ def test_nmf_mu_cache_follows_content(golden, monkeypatch):
     assert np.array_equal(again["h0"], fresh[0]["h0"])
 
 
+def test_nmf_mu_solo_cache_follows_content(golden):
+    """The solo path (k = 2 on the gct) keeps its device copy of A across calls only for the same A: A, A' (one
+    entry changed), A again give what a call after nmfc_nmf_mu_release (nothing cached) gives."""
+    from nmfconsensus_amd import _lib, libnmf
+    A = golden["A_gct"]
+    A2 = A.copy(order="F")
+    A2[517, 23] += 0.25
+    W0, H0 = golden["init_k2_W"], golden["init_k2_H"]
+    assert _lib.lib().nmfc_mu_solo_fits(A.shape[0], A.shape[1], 2)
+    cached = [libnmf.nmf_mu(X, W0, H0, 40) for X in (A, A2, A)]
+    fresh = []
+    for X in (A, A2):
+        _lib.lib().nmfc_nmf_mu_release()
+        fresh.append(libnmf.nmf_mu(X, W0, H0, 40))
+    for c, f in zip(cached, fresh + fresh[:1]):
+        assert np.array_equal(c["w0"], f["w0"]) and np.array_equal(c["h0"], f["h0"])
+    assert not np.array_equal(cached[0]["h0"], cached[1]["h0"])
+
+
 def test_nmf_mu_odd_iterations(golden, oracle):
     from nmfconsensus_amd import libnmf
     A = golden["A_gct"]
