@@ -53,7 +53,7 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
         subprocess.run(cmd, check=True, cwd=CSRC)
         objs.append(obj)
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
-           "-Wl,-soname,libnmf.so", "-Wl,-rpath,/opt/rocm/lib"]
+           "-Wl,-soname,libnmf.so", "-Wl,-rpath,/opt/rocm/lib", "-Wl,-z,defs"]   # an unresolved symbol fails the build
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

@@ -78,24 +78,32 @@ __device__ __forceinline__ double qbcast(double v, int b) {   // lane b of the q
 
 // SKIP != 0 only in tools/solobench.hip (phase costs): bit 0 no G / W^T W MFMAs, 1 no F / E / W rule, 2 no h h^T,
 // 3 no stop check, 4 no partial sums, 6 phase clock stamps of wave 0 into prof[1..7].
-template <int NCG, int KK, int SKIP = 0, int SBO = 0>
+// SL: the last SL gene steps of A live in LDS instead of registers (k >= 3 at n = 40: A's registers would spill)
+template <int NCG, int KK, int SKIP = 0, int SBO = 0, int SL = 0>
 __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restrict__ A, int m, int n,
                                                          double* __restrict__ W, double* __restrict__ H, int maxiter,
-                                                         int stop_rule, int* __restrict__ state,
+                                                         int stop_rule, int* __restrict__ state, int kt = KK,
                                                          long long* __restrict__ prof = nullptr) {
-  static_assert(4 * (KK * (SOLO_NMAX - 8 * (KK - 2)) + KK * KK) <= 64 * SOLO_W, "one quad per summed entry");
   // gene steps per F batch: larger means fewer H reads from LDS but more live registers (A holds most of them)
   constexpr int SB = SBO ? SBO : KK == 2 ? 8 : 4;
   __shared__ SoloSmem<NCG> sm;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, K = l >> 4, bq = (l >> 2) & 3, j = l & 3;
-  double a_[SOLO_S][NCG], w_[SOLO_S];
+  constexpr int SR = SOLO_S - SL;   // gene steps of A in registers
+  __shared__ double Al[SL > 0 ? SL : 1][NCG][64 * SOLO_W];   // steps SR.. of A, lane-contiguous
+  double a_[SR > 0 ? SR : 1][NCG], w_[SOLO_S];
+  // A[gene(s)][4 cg + j] from registers (s < SR) or LDS; s, cg compile-time after unrolling
+  auto av = [&](int s, int cg) -> double { return s < SR ? a_[s < SR ? s : 0][cg] : Al[s < SR ? 0 : s - SR][cg][tid]; };
 #pragma unroll
   for (int s = 0; s < SOLO_S; ++s) {
     const int g = 128 * w + 16 * s + 4 * bq + K;
 #pragma unroll
     for (int cg = 0; cg < NCG; ++cg) {
       const int c = 4 * cg + j;
-      a_[s][cg] = (g < m && c < n) ? A[(long)c * m + g] : 0.0;
+      const double v = (g < m && c < n) ? A[(long)c * m + g] : 0.0;
+      if (s < SR)
+        a_[s < SR ? s : 0][cg] = v;
+      else
+        Al[s < SR ? 0 : s - SR][cg][tid] = v;
     }
     w_[s] = (g < m && j < KK) ? W[(long)j * m + g] : 0.0;
   }
@@ -126,7 +134,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
 #pragma unroll
       for (int s = 0; s < ((SKIP & 1) ? 0 : SOLO_S); ++s) {
 #pragma unroll
-        for (int cg = 0; cg < NCG; ++cg) acc[cg] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s], a_[s][cg], acc[cg], 0, 0, 0);
+        for (int cg = 0; cg < NCG; ++cg) acc[cg] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s], av(s, cg), acc[cg], 0, 0, 0);
         acc[NCG] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s], w_[s], acc[NCG], 0, 0, 0);
       }
 #pragma unroll
@@ -139,8 +147,8 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
     // ---- sums: G (k x n) and W^T W (k x k), four threads per entry (a quad): lane p sums waves 2p, 2p + 1
     // (gene blocks b in order), then the quad butterfly ((p0 + p1) + (p2 + p3)) ----
     {
-      const int o = tid >> 2, p = tid & 3;
-      if (!(SKIP & 16) && o < KK * n + KK * KK) {   // whole quads in or out (DPP below)
+      const int p = tid & 3;
+      for (int o = tid >> 2; !(SKIP & 16) && o < KK * n + KK * KK; o += 16 * SOLO_W) {   // whole quads (DPP below)
         int a, c, cg, idx;
         if (o < KK * n) {
           a = o / n;
@@ -189,11 +197,12 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
         bool ch = false;
         if (stop_rule == nmfc::STOP_REF_COMPAT) {
           // window i reads the flat k x n column-major buffer at [i n, i n + k)
-          if (l < KK && l < n) {
+          // (kt: the restart's rank; KK = 4 > kt runs it with zero padding rows, which the rule never reads)
+          if (l < kt && l < n) {
             int cl = 0;
             double prev = 0.0;
-            for (int jj = 0; jj < KK; ++jj) {
-              const int f = l * n + jj, c = f / KK, a = f - c * KK;
+            for (int jj = 0; jj < kt; ++jj) {
+              const int f = l * n + jj, c = f / kt, a = f - c * kt;
               const double v = sm.Hc[hb][c][a];
               if (jj > 0 && v > prev) cl = jj;
               prev = v;
@@ -205,7 +214,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
           if (l < n) {
             int best = 0;
             double bv = sm.Hc[hb][l][0];
-            for (int a = 1; a < KK; ++a) {
+            for (int a = 1; a < kt; ++a) {
               const double v = sm.Hc[hb][l][a];
               if (v > bv) {
                 bv = v;
@@ -271,7 +280,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
         for (int q = 0; q < SB; ++q)
 #pragma unroll
           for (int a = 0; a < KK; ++a)   // the chain's first term is a product (fma onto +0 but for the zero's sign)
-            P[q][a] = cg == 0 ? a_[s0 + q][0] * h[a] : fma(a_[s0 + q][cg], h[a], P[q][a]);
+            P[q][a] = cg == 0 ? av(s0 + q, 0) * h[a] : fma(av(s0 + q, cg), h[a], P[q][a]);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int a = 0; a < KK; ++a) h[a] = hn[a];
@@ -338,9 +347,11 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
   }
 }
 
-template <int NCG, int KK>
-hipError_t launch(const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule, int* st, hipStream_t s) {
-  hipLaunchKernelGGL((k_solo_mu<NCG, KK>), dim3(1), dim3(64 * SOLO_W), 0, s, A, m, n, W, H, maxiter, stop_rule, st);
+template <int NCG, int KK, int SL = 0>
+hipError_t launch(const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule, int* st, int kt,
+                  hipStream_t s) {
+  hipLaunchKernelGGL((k_solo_mu<NCG, KK, 0, 0, SL>), dim3(1), dim3(64 * SOLO_W), 0, s, A, m, n, W, H, maxiter, stop_rule,
+                     st, kt, nullptr);
   return hipGetLastError();
 }
 
@@ -371,7 +382,6 @@ int fail(const char* what, hipError_t e) {
     if (e_ != hipSuccess) return fail(#x, e_);   \
   } while (0)
 
-// n <= 40 / 32 / 24 at k = 2 / 3 / 4: the kernels that keep A and their working set in registers without spilling
 // nmfc_nmf_mu_release (compat.hip): the device copy of A, the work buffer and the pinned staging
 extern "C" void nmfc_solo_release() {
   std::lock_guard<std::mutex> lock(g_lock);
@@ -385,8 +395,12 @@ extern "C" void nmfc_solo_release() {
   g.m = g.n = 0;
 }
 
+// every shape with 2 <= k <= 4, k <= m <= 1024, k <= n <= 40.  Kernels by (k, column groups of 4 samples):
+// A fully in registers where that does not spill (k = 2; k = 3 to n = 32; k = 4 to n = 24); else the last
+// steps of A in LDS (k = 4: one step to n = 32, two to n = 40) and k = 3 beyond n = 32 as k = 4 with a zero
+// padding row (the rows of a restart never mix, so its bits are those of the unpadded arithmetic)
 extern "C" int nmfc_mu_solo_fits(int m, int n, int k) {
-  return m >= k && n >= k && k >= 2 && k <= 4 && m <= SOLO_MMAX && n <= SOLO_NMAX - 8 * (k - 2);
+  return m >= k && n >= k && k >= 2 && k <= 4 && m <= SOLO_MMAX && n <= SOLO_NMAX;
 }
 
 extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, int stop_rule, const double* W0,
@@ -397,7 +411,9 @@ extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, i
     return -1;
   }
   std::lock_guard<std::mutex> lock(g_lock);
-  const size_t la = (size_t)m * n, lw = (size_t)m * k, lh = (size_t)k * n;
+  const int ncg = (n + 3) / 4;
+  const int kp = (k == 3 && ncg > 8) ? 4 : k;   // the kernel's rank (k = 3 padded to 4 at n > 32)
+  const size_t la = (size_t)m * n, lw = (size_t)m * kp, lh = (size_t)kp * n;
   if (!g.st) SCHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
   if (!(g.dA && g.m == m && g.n == n && memcmp(g.a->data(), A, la * sizeof(double)) == 0)) {
     if (g.dA) (void)hipFree(g.dA);
@@ -419,26 +435,34 @@ extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, i
     SCHECK(hipHostMalloc(&g.pin, need * sizeof(double), hipHostMallocDefault));
     g.cap = need;
   }
-  memcpy(g.pin + 2, W0, lw * sizeof(double));
-  memcpy(g.pin + 2 + lw, H0, lh * sizeof(double));
+  if (kp == k) {
+    memcpy(g.pin + 2, W0, lw * sizeof(double));
+    memcpy(g.pin + 2 + lw, H0, lh * sizeof(double));
+  } else {   // W0 m x k -> m x kp with zero columns, H0 k x n -> kp x n with zero rows
+    memcpy(g.pin + 2, W0, (size_t)m * k * sizeof(double));
+    memset(g.pin + 2 + (size_t)m * k, 0, (size_t)m * (kp - k) * sizeof(double));
+    for (int c = 0; c < n; ++c)
+      for (int a = 0; a < kp; ++a) g.pin[2 + lw + (size_t)c * kp + a] = a < k ? H0[(size_t)c * k + a] : 0.0;
+  }
   SCHECK(hipMemcpyAsync(g.dwork + 2, g.pin + 2, (lw + lh) * sizeof(double), hipMemcpyHostToDevice, g.st));
   int* dstate = reinterpret_cast<int*>(g.dwork);
   double* dW = g.dwork + 2;
   double* dH = dW + lw;
-  // samples in column groups of 4: NCG = 4, 6, 8, 10 groups (n <= 16, 24, 32, 40) by k (nmfc_mu_solo_fits)
-  const int ncg = (n + 3) / 4;
+  // samples in column groups of 4: NCG = 4, 6, 8, 10 groups (n <= 16, 24, 32, 40)
   const int gi = ncg <= 4 ? 0 : ncg <= 6 ? 1 : ncg <= 8 ? 2 : 3;
   hipError_t le;
-  switch (k * 4 + gi) {
-    case 8: le = launch<4, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
-    case 9: le = launch<6, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
-    case 10: le = launch<8, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
-    case 11: le = launch<10, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
-    case 12: le = launch<4, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
-    case 13: le = launch<6, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
-    case 14: le = launch<8, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
-    case 16: le = launch<4, 4>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
-    case 17: le = launch<6, 4>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, g.st); break;
+  switch (kp * 4 + gi) {
+    case 8: le = launch<4, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 9: le = launch<6, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 10: le = launch<8, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 11: le = launch<10, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 12: le = launch<4, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 13: le = launch<6, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 14: le = launch<8, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 16: le = launch<4, 4>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 17: le = launch<6, 4>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 18: le = launch<8, 4, 1>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
+    case 19: le = launch<10, 4, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
     default: nmfc_set_error("nmfc_mu_solo: internal shape dispatch"); return -1;
   }
   SCHECK(le);
@@ -446,8 +470,13 @@ extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, i
   SCHECK(hipStreamSynchronize(g.st));
   int hstate[2];
   memcpy(hstate, g.pin, sizeof hstate);
-  memcpy(W, g.pin + 2, lw * sizeof(double));
-  memcpy(H, g.pin + 2 + lw, lh * sizeof(double));
+  memcpy(W, g.pin + 2, (size_t)m * k * sizeof(double));   // the first k columns of the m x kp W
+  if (kp == k) {
+    memcpy(H, g.pin + 2 + lw, lh * sizeof(double));
+  } else {
+    for (int c = 0; c < n; ++c)
+      for (int a = 0; a < k; ++a) H[(size_t)c * k + a] = g.pin[2 + lw + (size_t)c * kp + a];
+  }
   if (iters) *iters = maxiter == 0 ? 0 : hstate[0];
   if (early) *early = hstate[1] == 1;
   return 0;

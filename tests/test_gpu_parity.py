@@ -554,10 +554,12 @@ def test_nmf_mu_team_failure_falls_back(golden, monkeypatch):
 
 
 @pytest.mark.parametrize("m,n,k", [(1000, 40, 2), (1024, 37, 2), (1000, 32, 3), (700, 24, 4), (640, 16, 2),
-                                   (37, 5, 4), (300, 29, 3), (129, 21, 4), (2, 9, 2)])
+                                   (37, 5, 4), (300, 29, 3), (129, 21, 4), (2, 9, 2),
+                                   (1000, 40, 3), (517, 37, 3), (1000, 40, 4), (1024, 30, 4), (3, 40, 3)])
 def test_solo_path_vs_oracle(oracle, m, n, k):
     """nmf_mu on one workgroup (nmfc_mu_solo, csrc/solo.hip: rank 2..4 on gct-sized matrices, A in one CU's
-    registers): fixed counts within 1e-9, the REF_COMPAT and ARGMAX_STABLE exits exact, ragged m and n."""
+    registers, its last gene steps in LDS for k = 4 at n > 24, k = 3 at n > 32 run padded to 4 rows): fixed
+    counts within 1e-9, the REF_COMPAT and ARGMAX_STABLE exits exact, ragged m and n."""
     import ctypes
     from nmfconsensus_amd import _lib
     L = _lib.lib()

@@ -15,7 +15,7 @@ void nmfc_set_error(const char* msg) { fprintf(stderr, "%s\n", msg); }
     }                                                                                       \
   } while (0)
 
-template <int NCG, int KK, int SBO = 0>
+template <int NCG, int KK, int SBO = 0, int SL = 0>
 void bench(int m, int n, int T, bool all = true) {
   std::vector<double> a((size_t)m * n), w((size_t)m * KK), h((size_t)KK * n);
   for (size_t i = 0; i < a.size(); ++i) a[i] = 0.05 + ((i * 7919) % 1000) / 1000.0;
@@ -33,14 +33,14 @@ void bench(int m, int n, int T, bool all = true) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  printf("k_solo_mu<%d, %d> (F batch %d) on %d x %d, %d FIXED iterations\n", NCG, KK, SBO, m, n, T);
+  printf("k_solo_mu<%d, %d> (F batch %d, A steps in LDS %d) on %d x %d, %d FIXED iterations\n", NCG, KK, SBO, SL, m, n, T);
   auto run = [&](auto kern, const char* name, bool stamps) {
     float best = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
       CK(hipMemcpy(dW, w.data(), w.size() * 8, hipMemcpyHostToDevice));
       CK(hipMemcpy(dH, h.data(), h.size() * 8, hipMemcpyHostToDevice));
       CK(hipEventRecord(e0));
-      hipLaunchKernelGGL(kern, dim3(1), dim3(64 * SOLO_W), 0, 0, dA, m, n, dW, dH, T, 0, st, prof);
+      hipLaunchKernelGGL(kern, dim3(1), dim3(64 * SOLO_W), 0, 0, dA, m, n, dW, dH, T, 0, st, KK, prof);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
@@ -61,7 +61,7 @@ void bench(int m, int n, int T, bool all = true) {
       printf(" sum %lld\n", tot / hs[0]);
     }
   };
-  run(k_solo_mu<NCG, KK, 0, SBO>, "full", false);
+  run(k_solo_mu<NCG, KK, 0, SBO, SL>, "full", false);
   if (!all) {
     CK(hipFree(dA));
     CK(hipFree(dW));
@@ -85,11 +85,10 @@ int main(int argc, char** argv) {
   bench<10, 2>(1000, 40, T);
   bench<8, 3>(1000, 32, T);
   bench<6, 4>(1000, 24, T);
-  // F batch size (gene steps per H re-read) against register pressure, and the gct at k = 3, 4
+  // the A-in-LDS kernels behind k = 4 at n > 24 and k = 3 at n > 32 (padded to 4), F batch variants
+  bench<8, 4, 0, 1>(1000, 32, T);
+  bench<10, 4, 0, 2>(1000, 40, T);
+  bench<10, 4, 2, 2>(1000, 40, T, false);
   bench<8, 3, 4>(1000, 32, T, false);
-  bench<6, 4, 1>(1000, 24, T, false);
-  bench<8, 4, 1>(1000, 32, T, false);
-  bench<10, 3, 1>(1000, 40, T, false);
-  bench<10, 4, 1>(1000, 40, T, false);
   return 0;
 }
