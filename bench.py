@@ -487,7 +487,7 @@ def bench_c1(args, dev):
                    "mean_iterations": float(its.mean()), "max_iterations": int(its.max())},
         "dropin_flow": {"value": len(jobs) / t_dropin, "unit": "restarts/s",
                         "what": "the 20 restarts through the drop-in nmf_mu one call after another (nmf.r's .C path "
-                                f"unchanged; per call k_solo_mu at k = 2, k_team_mu at k = 3..5); {t_dropin * 1e3:.1f} ms",
+                                f"unchanged; per call k_solo_mu at k = 2..4, k_team_mu at k = 5); {t_dropin * 1e3:.1f} ms",
                         "iterations_equal": bool(np.array_equal(np.asarray(dropin_its), its))},
         "roofline": roof, "cpu_baseline": cpu,
     }

@@ -110,9 +110,9 @@ int nmfc_engine_mu1(nmfc_engine* e, int k, int maxiter, int stop_rule, const dou
  * argument meaning as nmfc_engine_mu1 (W m x k, H k x n column-major, updated in place). */
 int nmfc_mu_generic(const double* A, int m, int n, int k, int maxiter, int stop_rule, double* W, double* H, int* iters,
                     int* early);
-/* One restart of nmf_mu of rank 2 <= k <= 4 on a small matrix (k <= m <= 1024; n <= 40 at k = 2, 32 at k = 3,
- * 24 at k = 4) on ONE workgroup: the whole MU loop and stop rule in one launch, A resident in that CU's registers
- * (csrc/solo.hip).  The drop-in's path for the bundled gct at k = 2.  W0/H0 in, W/H out (column-major, may alias),
+/* One restart of nmf_mu of rank 2 <= k <= 4 on a small matrix (k <= m <= 1024, k <= n <= 40) on ONE workgroup:
+ * the whole MU loop and stop rule in one launch, A resident in that CU's registers (and LDS) (csrc/solo.hip).
+ * The drop-in's path for the bundled gct at k = 2..4.  W0/H0 in, W/H out (column-major, may alias),
  * *iters / *early as nmfc_engine_mu1; A cached on the device across calls (compared byte for byte).  Returns 0, or
  * -1 (nmfc_last_error) for a shape outside the range (nmfc_mu_solo_fits says which shapes fit). */
 int nmfc_mu_solo_fits(int m, int n, int k);
