@@ -178,11 +178,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        # explicit timeout: a rank that dies makes the others exit non-zero instead of blocking in the all-reduce
+        from nmfconsensus_amd.distributed import init_distributed
+        init_distributed(args.dist_backend, dev)
 
     from nmfconsensus_amd.synthetic import CONFIGS, planted_matrix
     from nmfconsensus_amd.nmf import cophenetic_batch

@@ -97,7 +97,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                     const double* W_init, const double* H_init, nmfc_result* out);
 
 /* Convenience: create, run, destroy. */
-/* One restart of nmf_mu (nmf_mu.c:84-315) on the small-shape team kernel (m rounded up to 128 <= 1024, n <= 64,
+/* One restart of nmf_mu (nmf_mu.c:84-315) on the small-shape team kernel (m rounded up to 128 <= 8192, n <= 64,
  * k <= 16), with one upload, one launch and one download: the per-call path of the nmf_mu drop-in (nmf.r:41-45).
  * W0 (m x k) and H0 (k x n) column-major as nmf_mu takes them; W_out/H_out may alias them.  *iters = the
  * iterations run, *early = 1 when the stop rule (not maxiter) ended the loop.  stop_rule: FIXED, REF_COMPAT or

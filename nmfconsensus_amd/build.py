@@ -41,8 +41,9 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     if not force and not _stale(LIB, deps):
         return LIB
-    objs = []
-    for src in SOURCES:
+    from concurrent.futures import ThreadPoolExecutor
+
+    def compile_one(src):
         obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
         lang = [] if src.endswith(".hip") else ["-x", "c++"]
         off = [f"--offload-arch={ARCH}"] if src.endswith(".hip") else []
@@ -51,7 +52,11 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True, cwd=CSRC)
-        objs.append(obj)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "6"))))
+    with ThreadPoolExecutor(max_workers=jobs) as pool:   # one hipcc per translation unit, in parallel
+        objs = list(pool.map(compile_one, SOURCES))
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
            "-Wl,-soname,libnmf.so", "-Wl,-rpath,/opt/rocm/lib", "-Wl,-z,defs"]   # an unresolved symbol fails the build
     if verbose:

@@ -86,12 +86,22 @@ double randnumber(const int min, const int max) {
   return (double)min + ((double)prod / (double)(RAND_MAX));
 }
 
-// generatematrix.c:96-137 (ran); nndsvd (generatematrix.c:138-294) is out of scope -> ENOSYS
+// generatematrix.c:96-137 (ran); nndsvd (generatematrix.c:138-294) is out of scope -> ENOSYS.
+// The reference returns WITHOUT filling W/H whenever errno is non-zero on entry (generatematrix.c:86-90 under
+// ERROR_CHECKING, common.h:25: a stale errno from any earlier libc call is enough).  This entry point fills W/H
+// regardless (the caller asked for an init); NMFC_GENERATE_ERRNO_COMPAT=1 restores the reference's early return.
 void generateMatrix(const int* pm, const int* pn, const int* pk, init_t* pinit, const int* pmin, const int* pmax,
                     double* matrixW, double* matrixH, double* matrixA, options_t* opts) {
   (void)matrixA;
   (void)opts;
   const int m = *pm, n = *pn, k = *pk;
+  if (errno) {
+    const char* compat = getenv("NMFC_GENERATE_ERRNO_COMPAT");
+    if (compat && atoi(compat) != 0) {
+      perror("Failed to allocate memory in generateMatrix");
+      return;
+    }
+  }
   if (!matrixW || !matrixH) {
     // the reference mallocs a buffer the caller never sees (generatematrix.c:118-121)
     errno = EINVAL;

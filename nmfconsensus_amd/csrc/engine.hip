@@ -25,6 +25,12 @@
 
 using namespace nmfc;
 
+// solo.hip: the batched one-workgroup-per-restart kernel for rank <= 4 on gct-sized shapes
+int nmfc_solo_batch_rank(int n, int k);
+int nmfc_solo_batch_launch(const double* Acm, long a_ld, int m, int n, double* W, long w_ld, double* H, long h_ld,
+                           const nmfc::SoloJob* djobs, int njobs, int kp, int maxiter, int stop_rule, int* stop_iter,
+                           int* stop_reason, hipStream_t st);
+
 namespace {
 
 thread_local std::string g_err;
@@ -249,6 +255,30 @@ int live_panels(const Packing& pk) {
   return np;
 }
 
+// Small-shape path, restarts that the one-workgroup solo kernel takes (nmfc_mu_solo_fits(m, n, k): rank <= 4 on
+// gct-sized shapes): each gets 4 stacked columns of its own after the k_small_mu blocks (cols from col_base), in
+// order of kernel rank (one launch per rank), then restart id.  Returns the solo jobs; pk grows to hold them.
+std::vector<SoloJob> place_solo(Packing& pk, std::vector<RestartInfo> solo, int col_base, int n) {
+  std::stable_sort(solo.begin(), solo.end(), [n](const RestartInfo& a, const RestartInfo& b) {
+    const int ka = nmfc_solo_batch_rank(n, a.k), kb = nmfc_solo_batch_rank(n, b.k);
+    return ka != kb ? ka < kb : a.rid < b.rid;
+  });
+  std::vector<SoloJob> jobs;
+  int col = col_base;
+  for (RestartInfo r : solo) {
+    r.col0 = col;
+    col += 4;
+    pk.ri.push_back(r);
+    jobs.push_back(SoloJob{r.col0, r.k, r.rid, 0});
+  }
+  pk.npanels = std::max(pk.npanels, (col + PANEL - 1) / PANEL);
+  while (pk.npanels % WTA_NPT) ++pk.npanels;
+  pk.prb.assign(pk.npanels, 0);
+  pk.pre.assign(pk.npanels, 0);
+  pk.ci.assign((size_t)pk.npanels * PANEL, ColInfo{0, 0, 0, 0});
+  return jobs;
+}
+
 }  // namespace
 
 // error slot shared with the other translation units of the library (brunet.hip)
@@ -277,6 +307,10 @@ struct nmfc_engine {
   DevBuf prb, pre, colinfo, moves, finfo;
   DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp, smallblk;
   DevBuf teamG, teamSW, teamFlag;   // k_team_mu: partial buffers, per-workgroup flags (+ the error word)
+  DevBuf solojobs;                  // batched k_solo_mu jobs (small shapes, rank <= 4)
+  bool solo_ok = true;              // env NMFC_SOLO=0: no solo kernel (every small-shape restart in k_small_mu blocks)
+  hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // the solo launches (one per kernel rank) beside k_small_mu
+  hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
   int team_occ = 0;                // resident k_team_mu workgroups per CU (occupancy query, once)
   // nmfc_engine_mu1 (one restart, the nmf_mu drop-in): device and pinned staging [block | stop | W | H],
   // its own partial buffers and flags (zeroed when allocated; tags continue from mu1_base, the iterations of
@@ -559,6 +593,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_NARROW")) e->narrow_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_NARROW_MAXB")) e->narrow_maxb = std::min(8, std::max(1, atoi(s)));
   if (const char* s = getenv("NMFC_SMALL")) e->small_ok = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_SOLO")) e->solo_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SMALL_KERNEL"))
     e->small_kernel = std::string(s) == "team" ? 1 : std::string(s) == "single" ? 2 : 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
@@ -629,6 +664,12 @@ void nmfc_engine_destroy(nmfc_engine* e) {
                     &e->cons_tmp,  &e->Hstat,     &e->Wsnap,     &e->smallblk,  &e->teamG,    &e->teamSW,
                     &e->teamFlag,  &e->mu1_dev,   &e->mu1_G,     &e->mu1_SW,    &e->mu1_flag};
   for (DevBuf* b : bufs) b->release();
+  e->solojobs.release();
+  for (int q = 0; q < 3; ++q) {
+    if (e->aux[q]) (void)hipStreamDestroy(e->aux[q]);
+    if (e->join_ev[q]) (void)hipEventDestroy(e->join_ev[q]);
+  }
+  if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
   if (e->h_stopped) (void)hipHostFree(e->h_stopped);
   if (e->mu1_host) (void)hipHostFree(e->mu1_host);
   if (e->st) (void)hipStreamDestroy(e->st);
@@ -732,7 +773,14 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   // the stop rule only, so a job takes the same path -- and gives the same bits -- in any batch)
   const bool small = e->small_ok && e->m_pad <= 1024 && n <= 64 && opts.stop_rule != NMFC_STOP_TOLX;
   std::vector<SmallBlock> sblocks;
-  Packing pk = small ? pack_small(all, sblocks) : pack(all);
+  // ... and there, a restart the solo kernel takes (rank <= 4, nmfc_mu_solo_fits) runs on one workgroup of its own
+  // (k_solo_mu, the kernel of the single-restart drop-in), the others in k_small_mu blocks; the choice is a function
+  // of (m, n, k) only, so a job gives the same bits in any batch, through nmf_mu and on any number of GPUs
+  std::vector<RestartInfo> blk_jobs, solo_jobs;
+  for (const RestartInfo& r : all) (small && e->solo_ok && nmfc_mu_solo_fits(m, n, r.k) ? solo_jobs : blk_jobs).push_back(r);
+  Packing pk = small ? pack_small(blk_jobs, sblocks) : pack(all);
+  std::vector<SoloJob> solo;
+  if (small && !solo_jobs.empty()) solo = place_solo(pk, solo_jobs, (int)sblocks.size() * 16, n);
   const long cap_cols = (long)pk.npanels * PANEL;
   const int ntj = (int)(e->n_cols_pad / 128);
   const long g_ld = e->n_cols_pad;
@@ -883,14 +931,48 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   auto t_iter0 = std::chrono::steady_clock::now();
   int it = 0, q = 0, checked = 0;
   if (small) {
-    if (e->smallblk.ensure(sizeof(SmallBlock) * sblocks.size())) return -1;
-    HCHECK(hipMemcpyAsync(e->smallblk.p, sblocks.data(), sizeof(SmallBlock) * sblocks.size(), hipMemcpyHostToDevice, st));
+    if (!sblocks.empty()) {
+      if (e->smallblk.ensure(sizeof(SmallBlock) * sblocks.size())) return -1;
+      HCHECK(hipMemcpyAsync(e->smallblk.p, sblocks.data(), sizeof(SmallBlock) * sblocks.size(), hipMemcpyHostToDevice, st));
+    }
+    if (!solo.empty()) {
+      if (e->solojobs.ensure(sizeof(SoloJob) * solo.size())) return -1;
+      HCHECK(hipMemcpyAsync(e->solojobs.p, solo.data(), sizeof(SoloJob) * solo.size(), hipMemcpyHostToDevice, st));
+      for (int q = 0; q < 3; ++q) {
+        if (!e->aux[q]) HCHECK(hipStreamCreateWithFlags(&e->aux[q], hipStreamNonBlocking));
+        if (!e->join_ev[q]) HCHECK(hipEventCreateWithFlags(&e->join_ev[q], hipEventDisableTiming));
+      }
+      if (!e->fork_ev) HCHECK(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
+    }
     {
-      TimedLaunch tl(e, KID_SMALL);
-      if (launch_small(e, (int)sblocks.size(), opts.maxiter, opts.stop_rule)) return -1;
+      TimedLaunch tl(e, KID_SMALL);   // the whole small-shape phase: k_small_mu blocks and the solo launches
+      const bool team = use_team(e, (int)sblocks.size());
+      if (!sblocks.empty() && launch_small(e, (int)sblocks.size(), opts.maxiter, opts.stop_rule)) return -1;
+      if (!solo.empty()) {
+        // beside k_small_mu on streams of their own (one launch per kernel rank), after it when teams run (a team's
+        // workgroups must all be resident at once: nothing else may hold CUs then)
+        HCHECK(hipEventRecord(e->fork_ev, st));
+        size_t g0 = 0;
+        for (int q = 0; g0 < solo.size(); ++q) {
+          const int kp = nmfc_solo_batch_rank(n, solo[g0].k);
+          size_t g1 = g0;
+          while (g1 < solo.size() && nmfc_solo_batch_rank(n, solo[g1].k) == kp) ++g1;
+          hipStream_t sq = team ? st : e->aux[q];
+          if (!team) HCHECK(hipStreamWaitEvent(sq, e->fork_ev, 0));
+          if (nmfc_solo_batch_launch(e->Acm.as<double>(), e->m_pad, m, n, e->W[0].as<double>(), e->m_pad,
+                                     e->H[0].as<double>(), e->n_pad, e->solojobs.as<SoloJob>() + g0, (int)(g1 - g0), kp,
+                                     opts.maxiter, opts.stop_rule, e->stop_iter.as<int>(), e->stop_reason.as<int>(), sq))
+            return -1;
+          if (!team) {
+            HCHECK(hipEventRecord(e->join_ev[q], sq));
+            HCHECK(hipStreamWaitEvent(st, e->join_ev[q], 0));
+          }
+          g0 = g1;
+        }
+      }
     }
     HCHECK(hipStreamSynchronize(st));
-    if (use_team(e, (int)sblocks.size()) && team_failed(e, (int)sblocks.size())) {
+    if (!sblocks.empty() && use_team(e, (int)sblocks.size()) && team_failed(e, (int)sblocks.size())) {
       set_err("k_team_mu: a team of workgroups could not meet (not co-resident?)");
       return -1;
     }

@@ -4,10 +4,14 @@
 // multiplicative rules (nmf_mu.c:184-191, 209-216) and the stability check (nmf_mu.c:253-282) as small kernels.
 // Layouts are the reference's: A m x n, W m x k, H k x n, all column-major.  A rare path (consensus clustering
 // sweeps k = 2..10 or so); the fast paths are the team kernel and the batched engine (engine.hip).
+// Cost: W^T A runs k n threads, each a serial chain over all m genes, and an iteration is 9 dependent launches, so on a
+// large matrix (e.g. 60000 x 2000 at k = 20: 40000 threads x 60000 dependent fmas) one iteration takes on the order of
+// milliseconds -- correct and deterministic, not fast.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -108,10 +112,34 @@ struct GenCache {   // device copy of the last A (compared byte for byte) and wo
   double* work = nullptr;
   size_t work_bytes = 0;
   int* state = nullptr;
+  int* cls = nullptr;   // the stability check's classes (n of them)
+  int cls_n = 0;
   hipStream_t st = nullptr;
+  int dev = -1;         // the HIP device every resource above lives on
 };
 std::mutex g_lock;
 GenCache g;
+
+void cache_drop() {   // g_lock held
+  if (g.st) (void)hipStreamSynchronize(g.st);
+  if (g.dA) (void)hipFree(g.dA);
+  if (g.work) (void)hipFree(g.work);
+  if (g.state) (void)hipFree(g.state);
+  if (g.cls) (void)hipFree(g.cls);
+  if (g.st) (void)hipStreamDestroy(g.st);
+  g.a.clear();
+  g.a.shrink_to_fit();
+  g.dA = g.work = nullptr;
+  g.state = g.cls = nullptr;
+  g.st = nullptr;
+  g.work_bytes = 0;
+  g.cls_n = 0;
+  g.m = g.n = 0;
+  g.dev = -1;
+}
+
+int mu_generic_call(const double* A, int m, int n, int k, int maxiter, int stop_rule, double* W, double* H, int* iters,
+                    int* early);
 
 int fail(const char* what, hipError_t e) {
   char buf[256];
@@ -136,6 +164,22 @@ extern "C" int nmfc_mu_generic(const double* A, int m, int n, int k, int maxiter
     return -1;
   }
   std::lock_guard<std::mutex> lock(g_lock);
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return fail("hipGetDevice", hipErrorInvalidDevice);
+  if (g.dev >= 0 && g.dev != dev) cache_drop();
+  const int rc = mu_generic_call(A, m, n, k, maxiter, stop_rule, W, H, iters, early);
+  // a failed call may leave a half-done upload behind: nothing of it is reused; NMFC_NMF_MU_CACHE=0 keeps nothing
+  const char* env = getenv("NMFC_NMF_MU_CACHE");
+  if (rc != 0 || (env && atoi(env) == 0))
+    cache_drop();
+  else
+    g.dev = dev;
+  return rc;
+}
+
+namespace {
+int mu_generic_call(const double* A, int m, int n, int k, int maxiter, int stop_rule, double* W, double* H, int* iters,
+                    int* early) {
   const size_t la = (size_t)m * n;
   if (!g.st) GCHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
   if (!(g.dA && g.m == m && g.n == n && memcmp(g.a.data(), A, la * sizeof(double)) == 0)) {
@@ -166,8 +210,14 @@ extern "C" int nmfc_mu_generic(const double* A, int m, int n, int k, int maxiter
   double* denh = numh + lh;
   double* wtw = denh + lh;
   double* hht = wtw + lk;
-  int* cls = nullptr;
-  GCHECK(hipMallocAsync((void**)&cls, sizeof(int) * (size_t)n, g.st));
+  if (g.cls_n < n) {
+    if (g.cls) (void)hipFree(g.cls);
+    g.cls = nullptr;
+    g.cls_n = 0;
+    GCHECK(hipMalloc(&g.cls, sizeof(int) * (size_t)n));
+    g.cls_n = n;
+  }
+  int* cls = g.cls;
   GCHECK(hipMemsetAsync(cls, 0, sizeof(int) * (size_t)n, g.st));   // nmf_mu.c:132
   GCHECK(hipMemsetAsync(g.state, 0, sizeof(int) * 8, g.st));
   GCHECK(hipMemcpyAsync(dW, W, lw * sizeof(double), hipMemcpyHostToDevice, g.st));
@@ -206,9 +256,9 @@ extern "C" int nmfc_mu_generic(const double* A, int m, int n, int k, int maxiter
   GCHECK(hipMemcpyAsync(W, dW, lw * sizeof(double), hipMemcpyDeviceToHost, g.st));
   GCHECK(hipMemcpyAsync(H, dH, lh * sizeof(double), hipMemcpyDeviceToHost, g.st));
   GCHECK(hipMemcpyAsync(hstate, g.state, sizeof(int) * 4, hipMemcpyDeviceToHost, g.st));
-  GCHECK(hipFreeAsync(cls, g.st));
   GCHECK(hipStreamSynchronize(g.st));
   if (iters) *iters = maxiter == 0 ? 0 : hstate[1];
   if (early) *early = hstate[2] == 1;
   return 0;
 }
+}  // namespace

@@ -1101,6 +1101,12 @@ struct SmallBlock {
   int lc0[SMALL_MAXR];       // block-local first column
 };
 
+// One restart of a batched k_solo_mu launch (csrc/solo.hip; rank <= 4 on gct-sized shapes): its stacked W/H
+// rows col0 .. col0 + k - 1 and its persistent restart id (stop iteration / reason slots).
+struct SoloJob {
+  int col0, k, rid, pad;
+};
+
 template <int JB>
 struct SmallSmem {
   double H[16][16 * JB];           // current H of the block (rows = columns c)

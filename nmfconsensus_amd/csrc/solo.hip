@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -79,15 +80,35 @@ __device__ __forceinline__ double qbcast(double v, int b) {   // lane b of the q
 // SKIP != 0 only in tools/solobench.hip (phase costs): bit 0 no G / W^T W MFMAs, 1 no F / E / W rule, 2 no h h^T,
 // 3 no stop check, 4 no partial sums, 6 phase clock stamps of wave 0 into prof[1..7].
 // SL: the last SL gene steps of A live in LDS instead of registers (k >= 3 at n = 40: A's registers would spill)
+// Operand layout of a launch.  One restart (nmfc_mu_solo): A m x n column-major (a_ld = m), W m x KK (w_ld = m),
+// H KK x n column-major (h_sc = KK, h_sa = 1), the stop state in state[0..1].  A batch (nmfc_engine_run, one
+// workgroup per restart): A = the engine's column-major Acm (a_ld = m_pad), W/H the stacked [cols][m_pad] /
+// [cols][n_pad] buffers at each job's col0 (w_ld = m_pad, h_sc = 1, h_sa = n_pad), the stop state in
+// stop_iter / stop_reason[rid].  Only pointers and strides differ: every arithmetic step is the same code.
+struct SoloLayout {
+  long a_ld, w_ld, h_sc, h_sa;
+  const nmfc::SoloJob* jobs;   // nullptr: one restart
+  int* stop_iter;
+  int* stop_reason;
+};
+
 template <int NCG, int KK, int SKIP = 0, int SBO = 0, int SL = 0>
 __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restrict__ A, int m, int n,
                                                          double* __restrict__ W, double* __restrict__ H, int maxiter,
-                                                         int stop_rule, int* __restrict__ state, int kt = KK,
-                                                         long long* __restrict__ prof = nullptr) {
+                                                         int stop_rule, int* __restrict__ state, int kt,
+                                                         long long* __restrict__ prof, SoloLayout lay) {
   // gene steps per F batch: larger means fewer H reads from LDS but more live registers (A holds most of them)
   constexpr int SB = SBO ? SBO : KK == 2 ? 8 : 4;
   __shared__ SoloSmem<NCG> sm;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, K = l >> 4, bq = (l >> 2) & 3, j = l & 3;
+  int rid = -1;
+  if (lay.jobs) {   // batched: this workgroup's restart
+    const nmfc::SoloJob jb = lay.jobs[blockIdx.x];
+    W += (long)jb.col0 * lay.w_ld;
+    H += (long)jb.col0 * lay.h_sa;
+    kt = jb.k;
+    rid = jb.rid;
+  }
   constexpr int SR = SOLO_S - SL;   // gene steps of A in registers
   __shared__ double Al[SL > 0 ? SL : 1][NCG][64 * SOLO_W];   // steps SR.. of A, lane-contiguous
   double a_[SR > 0 ? SR : 1][NCG], w_[SOLO_S];
@@ -99,13 +120,13 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
 #pragma unroll
     for (int cg = 0; cg < NCG; ++cg) {
       const int c = 4 * cg + j;
-      const double v = (g < m && c < n) ? A[(long)c * m + g] : 0.0;
+      const double v = (g < m && c < n) ? A[(long)c * lay.a_ld + g] : 0.0;
       if (s < SR)
         a_[s < SR ? s : 0][cg] = v;
       else
         Al[s < SR ? 0 : s - SR][cg][tid] = v;
     }
-    w_[s] = (g < m && j < KK) ? W[(long)j * m + g] : 0.0;
+    w_[s] = (g < m && j < kt) ? W[(long)j * lay.w_ld + g] : 0.0;   // rows kt .. KK - 1: zero padding
   }
   for (int x = tid; x < 2 * SOLO_NCOLP * 4; x += 64 * SOLO_W) (&sm.Hc[0][0][0])[x] = 0.0;
   if (tid == 0) {
@@ -113,7 +134,10 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
     sm.reason = 0;
   }
   __syncthreads();
-  for (int x = tid; x < KK * n; x += 64 * SOLO_W) sm.Hc[0][x / KK][x % KK] = H[x];   // H is k x n column-major
+  for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
+    const int c = x / kt, a = x - c * kt;
+    sm.Hc[0][c][a] = H[(long)c * lay.h_sc + (long)a * lay.h_sa];
+  }
   __syncthreads();
   long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = 0;
 #define SOLO_STAMP(i)                                             \
@@ -338,21 +362,54 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
 #pragma unroll
   for (int s = 0; s < SOLO_S; ++s) {
     const int g = 128 * w + 16 * s + 4 * bq + K;
-    if (g < m && j < KK) W[(long)j * m + g] = w_[s];
+    if (g < m && j < kt) W[(long)j * lay.w_ld + g] = w_[s];
   }
-  for (int x = tid; x < KK * n; x += 64 * SOLO_W) H[x] = sm.Hc[hb][x / KK][x % KK];
+  for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
+    const int c = x / kt, a = x - c * kt;
+    H[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][a];
+  }
   if (tid == 0) {
-    state[0] = sm.stop;
-    state[1] = sm.reason;
+    if (rid >= 0) {
+      lay.stop_iter[rid] = sm.stop;
+      lay.stop_reason[rid] = sm.reason;
+    } else {
+      state[0] = sm.stop;
+      state[1] = sm.reason;
+    }
   }
 }
 
 template <int NCG, int KK, int SL = 0>
-hipError_t launch(const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule, int* st, int kt,
-                  hipStream_t s) {
-  hipLaunchKernelGGL((k_solo_mu<NCG, KK, 0, 0, SL>), dim3(1), dim3(64 * SOLO_W), 0, s, A, m, n, W, H, maxiter, stop_rule,
-                     st, kt, nullptr);
+hipError_t launch(int grid, const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule, int* st,
+                  int kt, const SoloLayout& lay, hipStream_t s) {
+  hipLaunchKernelGGL((k_solo_mu<NCG, KK, 0, 0, SL>), dim3(grid), dim3(64 * SOLO_W), 0, s, A, m, n, W, H, maxiter,
+                     stop_rule, st, kt, nullptr, lay);
   return hipGetLastError();
+}
+
+// the kernel rank for (n, k): k = 3 beyond n = 32 runs as k = 4 with a zero padding row
+int solo_rank(int n, int k) { return (k == 3 && (n + 3) / 4 > 8) ? 4 : k; }
+
+// the (column groups, rank, A steps in LDS) instantiation for (n, kernel rank kp); grid workgroups
+hipError_t dispatch(int grid, int kp, const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule,
+                    int* st, int kt, const SoloLayout& lay, hipStream_t s) {
+  // samples in column groups of 4: NCG = 4, 6, 8, 10 groups (n <= 16, 24, 32, 40)
+  const int ncg = (n + 3) / 4;
+  const int gi = ncg <= 4 ? 0 : ncg <= 6 ? 1 : ncg <= 8 ? 2 : 3;
+  switch (kp * 4 + gi) {
+    case 8: return launch<4, 2>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 9: return launch<6, 2>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 10: return launch<8, 2>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 11: return launch<10, 2>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 12: return launch<4, 3>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 13: return launch<6, 3>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 14: return launch<8, 3>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 16: return launch<4, 4>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 17: return launch<6, 4>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 18: return launch<8, 4, 1>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    case 19: return launch<10, 4, 2>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 struct SoloCache {   // device copy of the last A (compared byte for byte), work buffer, pinned staging
@@ -363,9 +420,25 @@ struct SoloCache {   // device copy of the last A (compared byte for byte), work
   double* pin = nullptr;     // pinned image of dwork
   size_t cap = 0;            // doubles in dwork / pin
   hipStream_t st = nullptr;
+  int dev = -1;              // the HIP device every resource above lives on
 };
 std::mutex g_lock;
 SoloCache g;
+
+void cache_drop() {   // g_lock held: frees everything, so the next call starts from scratch
+  if (g.st) (void)hipStreamSynchronize(g.st);
+  if (g.dA) (void)hipFree(g.dA);
+  if (g.dwork) (void)hipFree(g.dwork);
+  if (g.pin) (void)hipHostFree(g.pin);
+  if (g.st) (void)hipStreamDestroy(g.st);
+  delete g.a;
+  g.a = nullptr;
+  g.dA = g.dwork = g.pin = nullptr;
+  g.st = nullptr;
+  g.cap = 0;
+  g.m = g.n = 0;
+  g.dev = -1;
+}
 
 int fail(const char* what, hipError_t e) {
   char buf[256];
@@ -385,14 +458,7 @@ int fail(const char* what, hipError_t e) {
 // nmfc_nmf_mu_release (compat.hip): the device copy of A, the work buffer and the pinned staging
 extern "C" void nmfc_solo_release() {
   std::lock_guard<std::mutex> lock(g_lock);
-  if (g.dA) (void)hipFree(g.dA);
-  if (g.dwork) (void)hipFree(g.dwork);
-  if (g.pin) (void)hipHostFree(g.pin);
-  delete g.a;
-  g.a = nullptr;
-  g.dA = g.dwork = g.pin = nullptr;
-  g.cap = 0;
-  g.m = g.n = 0;
+  cache_drop();
 }
 
 // every shape with 2 <= k <= 4, k <= m <= 1024, k <= n <= 40.  Kernels by (k, column groups of 4 samples):
@@ -403,6 +469,14 @@ extern "C" int nmfc_mu_solo_fits(int m, int n, int k) {
   return m >= k && n >= k && k >= 2 && k <= 4 && m <= SOLO_MMAX && n <= SOLO_NMAX;
 }
 
+namespace {
+int mu_solo_call(const double* A, int m, int n, int k, int maxiter, int stop_rule, const double* W0, const double* H0,
+                 double* W, double* H, int* iters, int* early);
+}
+
+// The device copy of A, the work buffer, the pinned staging and the stream are kept across calls (nmf.r calls
+// nmf_mu once per restart on one matrix) on the device of the call that made them: a call on another device, a
+// failed call (nothing cached may hold a half-done upload) and NMFC_NMF_MU_CACHE=0 (after the call) free them.
 extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, int stop_rule, const double* W0,
                             const double* H0, double* W, double* H, int* iters, int* early) {
   if (!A || !W0 || !H0 || !W || !H || !nmfc_mu_solo_fits(m, n, k) || maxiter < 0 ||
@@ -411,8 +485,22 @@ extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, i
     return -1;
   }
   std::lock_guard<std::mutex> lock(g_lock);
-  const int ncg = (n + 3) / 4;
-  const int kp = (k == 3 && ncg > 8) ? 4 : k;   // the kernel's rank (k = 3 padded to 4 at n > 32)
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return fail("hipGetDevice", hipErrorInvalidDevice);
+  if (g.dev >= 0 && g.dev != dev) cache_drop();
+  const int rc = mu_solo_call(A, m, n, k, maxiter, stop_rule, W0, H0, W, H, iters, early);
+  const char* env = getenv("NMFC_NMF_MU_CACHE");
+  if (rc != 0 || (env && atoi(env) == 0))
+    cache_drop();
+  else
+    g.dev = dev;
+  return rc;
+}
+
+namespace {
+int mu_solo_call(const double* A, int m, int n, int k, int maxiter, int stop_rule, const double* W0, const double* H0,
+                 double* W, double* H, int* iters, int* early) {
+  const int kp = solo_rank(n, k);   // the kernel's rank (k = 3 padded to 4 at n > 32)
   const size_t la = (size_t)m * n, lw = (size_t)m * kp, lh = (size_t)kp * n;
   if (!g.st) SCHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
   if (!(g.dA && g.m == m && g.n == n && memcmp(g.a->data(), A, la * sizeof(double)) == 0)) {
@@ -448,24 +536,8 @@ extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, i
   int* dstate = reinterpret_cast<int*>(g.dwork);
   double* dW = g.dwork + 2;
   double* dH = dW + lw;
-  // samples in column groups of 4: NCG = 4, 6, 8, 10 groups (n <= 16, 24, 32, 40)
-  const int gi = ncg <= 4 ? 0 : ncg <= 6 ? 1 : ncg <= 8 ? 2 : 3;
-  hipError_t le;
-  switch (kp * 4 + gi) {
-    case 8: le = launch<4, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 9: le = launch<6, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 10: le = launch<8, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 11: le = launch<10, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 12: le = launch<4, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 13: le = launch<6, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 14: le = launch<8, 3>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 16: le = launch<4, 4>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 17: le = launch<6, 4>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 18: le = launch<8, 4, 1>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    case 19: le = launch<10, 4, 2>(g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, g.st); break;
-    default: nmfc_set_error("nmfc_mu_solo: internal shape dispatch"); return -1;
-  }
-  SCHECK(le);
+  const SoloLayout lay{m, m, kp, 1, nullptr, nullptr, nullptr};
+  SCHECK(dispatch(1, kp, g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, lay, g.st));
   SCHECK(hipMemcpyAsync(g.pin, g.dwork, need * sizeof(double), hipMemcpyDeviceToHost, g.st));
   SCHECK(hipStreamSynchronize(g.st));
   int hstate[2];
@@ -479,5 +551,26 @@ extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, i
   }
   if (iters) *iters = maxiter == 0 ? 0 : hstate[0];
   if (early) *early = hstate[1] == 1;
+  return 0;
+}
+}  // namespace
+
+// Batched form (nmfc_engine_run, small shapes): one workgroup per job of kernel rank kp (solo_rank(n, k) == kp for
+// every job; the engine groups its solo jobs by kp), reading the engine's column-major Acm and the stacked W/H at
+// each job's col0, stop state into stop_iter / stop_reason[rid].  Returns 0 or -1 (nmfc_last_error).
+__attribute__((visibility("hidden"))) int nmfc_solo_batch_rank(int n, int k) { return solo_rank(n, k); }
+
+__attribute__((visibility("hidden"))) int nmfc_solo_batch_launch(const double* Acm, long a_ld, int m, int n, double* W,
+                                                                 long w_ld, double* H, long h_ld,
+                                                                 const nmfc::SoloJob* djobs, int njobs, int kp,
+                                                                 int maxiter, int stop_rule, int* stop_iter,
+                                                                 int* stop_reason, hipStream_t st) {
+  if (njobs <= 0) return 0;
+  if (!nmfc_mu_solo_fits(m, n, 2) || kp < 2 || kp > 4) {
+    nmfc_set_error("nmfc_solo_batch_launch: shape outside the solo kernel's range");
+    return -1;
+  }
+  const SoloLayout lay{a_ld, w_ld, 1, h_ld, djobs, stop_iter, stop_reason};
+  SCHECK(dispatch(njobs, kp, Acm, m, n, W, H, maxiter, stop_rule, nullptr, kp, lay, st));
   return 0;
 }

@@ -22,6 +22,30 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 
+DEFAULT_TIMEOUT_S = 300.0
+
+
+def init_distributed(backend: str = "nccl", device=None, timeout_s: float | None = None):
+    """torch.distributed.init_process_group with an explicit timeout (failure containment).  A rank that dies
+    (or never arrives) makes the others leave the rendezvous or the counts all-reduce with an error after
+    timeout_s instead of blocking until the backend's default (10 min NCCL / 30 min gloo): they exit non-zero.
+    timeout_s defaults to $NMFC_DIST_TIMEOUT_S or 300 s, far above the largest shard imbalance of a sweep
+    (seconds) and the first `import torch` on a fresh box.  backend "nccl" is RCCL on ROCm; device: the rank's
+    torch.device (binds the communicator to it)."""
+    import datetime
+    import os
+
+    import torch.distributed as dist
+
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("NMFC_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+    kw = {"timeout": datetime.timedelta(seconds=timeout_s)}
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend, **kw)
+    return timeout_s
+
+
 def shard_range(njobs: int, rank: int, world: int):
     """Contiguous near-equal split of units [0, njobs)."""
     base, rem = divmod(njobs, world)

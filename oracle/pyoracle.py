@@ -167,7 +167,10 @@ class RefLib:
     def __init__(self, path: str = REF_SO):
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: run `make -C oracle ref` (needs /root/reference)")
-        L = ctypes.CDLL(path, mode=os.RTLD_LAZY)
+        # use_errno: the reference's generateMatrix returns early, leaving W/H untouched, whenever errno is
+        # non-zero on entry (generatematrix.c:86-90 under ERROR_CHECKING, common.h:25); generate_ran clears
+        # the ctypes-private errno before every call and checks that W/H came back filled.
+        L = ctypes.CDLL(path, mode=os.RTLD_LAZY, use_errno=True)
         ip = ctypes.POINTER(ctypes.c_int)
         L.nmf_mu.argtypes = [_dp, _dp, _dp, ip, ip, ip, ip, _dp, _dp]
         L.nmf_mu.restype = ctypes.c_double
@@ -195,8 +198,12 @@ class RefLib:
         H = np.zeros((k, n), dtype=np.float64, order="F")
         c = ctypes.c_int
         init = c(0)  # ran
+        ctypes.set_errno(0)
         self.L.generateMatrix(ctypes.byref(c(m)), ctypes.byref(c(n)), ctypes.byref(c(k)), ctypes.byref(init),
                               ctypes.byref(c(lo)), ctypes.byref(c(hi)), _d(W), _d(H), None, None)
+        if not (W.any() and H.any()):
+            raise RuntimeError(f"reference generateMatrix left W/H unfilled (errno {ctypes.get_errno()} on return; "
+                               "generatematrix.c:86-90 returns early when errno is set on entry)")
         return W, H
 
     def nmf_mu(self, A, W, H, maxiter: int, tol: float = 1e-4):

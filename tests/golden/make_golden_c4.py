@@ -2,13 +2,14 @@
 """Generates tests/golden/golden_c4.npz from the REFERENCE's own nmf_mu (TEST INFRASTRUCTURE ONLY).
 
 Run in the build container (needs /root/reference):
-    make -C oracle ref && python tests/golden/make_golden_c4.py [R] [procs]
+    make -C oracle ref && python tests/golden/make_golden_c4.py [R] [procs] [T]
 
 BASELINE configs[3] (C4): synthetic 60000 x 2000 (nmfconsensus_amd.synthetic.planted_matrix; A is 960 MB
 and is NOT stored -- its SHA-256 is, and the GPU test refuses to compare against a different A),
 k = 2..15, the first R restarts of every k (default 2: jobs 0..27 of the C4 grid, which rank 0's shard of
-the 8-GPU job and the bench's per-GPU C4 shard both start with), seed 123, jobs in expand.grid order
-(k fastest, nmf.r:63-68), job
+the 8-GPU job and the bench's per-GPU C4 shard both start with) plus the LAST T restarts of every k of the
+full 1000-restart grid (default 1: jobs 13986..13999, the end of rank 7's shard), seed 123, jobs in
+expand.grid order (k fastest, nmf.r:63-68), job
 seed = seed + job_id - 1, init = the reference's generateMatrix(ran) after srand(job seed), REF_COMPAT
 exit (nmf_mu.c:253-282), maxiter 10000 (nmf.r:13).  Every job runs through oracle/_ref/libnmf_ref.so
 (the reference's libnmf sources compiled out-of-tree by oracle/Makefile, never copied) with
@@ -36,7 +37,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden_c4.npz")
 CKPT = "/tmp/golden_c4_ckpt.npz"
-M, N, KS, SEED = 60000, 2000, list(range(2, 16)), 123
+M, N, KS, SEED, R_TOTAL = 60000, 2000, list(range(2, 16)), 123, 1000
 
 _A = None
 
@@ -72,16 +73,15 @@ def _margin(H: np.ndarray, largest: bool) -> float:
 def main():
     R = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     procs = int(sys.argv[2]) if len(sys.argv) > 2 else min(7, os.cpu_count() or 1)
+    T = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     from nmfconsensus_amd.synthetic import planted_matrix
     A = planted_matrix(M, N)
     a_sha = hashlib.sha256(np.ascontiguousarray(A).tobytes(order="F")).hexdigest()
     del A
-    jobs = []
-    jid = 0
-    for r in range(1, R + 1):
-        for k in KS:
-            jid += 1
-            jobs.append((jid - 1, k, SEED + jid - 1))
+    # (position in the golden, global job id, k, seed): restarts r = 1..R and r = R_TOTAL-T+1..R_TOTAL
+    rs = list(range(1, R + 1)) + list(range(R_TOTAL - T + 1, R_TOTAL + 1))
+    gids = [(r - 1) * len(KS) + i for r in rs for i in range(len(KS))]
+    jobs = [(p, KS[g % len(KS)], SEED + g) for p, g in enumerate(gids)]
     nj = len(jobs)
     iters = np.full(nj, -1, dtype=np.int32)
     lam = np.zeros((nj, N), dtype=np.int8)
@@ -92,23 +92,28 @@ def main():
     if os.path.exists(CKPT):
         with np.load(CKPT, allow_pickle=False) as c:
             if str(c["a_sha"]) == a_sha:
-                n0 = min(nj, c["iters"].shape[0])
-                iters[:n0], lam[:n0], lro[:n0] = c["iters"][:n0], c["lam"][:n0], c["lro"][:n0]
-                mam[:n0], mro[:n0] = c["mam"][:n0], c["mro"][:n0]
-                for key in c.files:
-                    if key.startswith("H_"):
-                        Hkeep[int(key[2:])] = c[key]
+                # positions are matched by global job id (older checkpoints hold jobs 0..n0-1 only)
+                old_ids = c["gids"] if "gids" in c.files else np.arange(c["iters"].shape[0])
+                pos = {int(g): q for q, g in enumerate(old_ids)}
+                for p, g in enumerate(gids):
+                    if g in pos:
+                        q = pos[g]
+                        iters[p], lam[p], lro[p], mam[p], mro[p] = (c["iters"][q], c["lam"][q], c["lro"][q],
+                                                                    c["mam"][q], c["mro"][q])
+                        if f"H_{q}" in c.files:
+                            Hkeep[p] = c[f"H_{q}"]
     todo = [j for j in jobs if iters[j[0]] < 0]
     print(f"C4 golden: {nj} jobs, {nj - len(todo)} from checkpoint, {procs} processes", file=sys.stderr)
     keep_jobs = set()
-    for k in KS:
-        keep_jobs.update([j for j, kk, _ in jobs if kk == k][:1])
+    for k in KS:   # the final H of the first and (with T > 0) the last job of every k
+        sel = [j for j, kk, _ in jobs if kk == k]
+        keep_jobs.update([sel[0], sel[-1]])
     t0 = time.time()
     done = 0
 
     def ckpt():
         extra = {f"H_{j}": h for j, h in Hkeep.items()}
-        np.savez(CKPT, a_sha=a_sha, iters=iters, lam=lam, lro=lro, mam=mam, mro=mro, **extra)
+        np.savez(CKPT, a_sha=a_sha, gids=np.array(gids), iters=iters, lam=lam, lro=lro, mam=mam, mro=mro, **extra)
 
     with mp.get_context("spawn").Pool(procs, initializer=_init_worker) as pool:
         for j, it, H in pool.imap_unordered(_job, todo, chunksize=1):
@@ -128,10 +133,11 @@ def main():
     ckpt()
     job_k = np.array([k for _, k, _ in jobs], dtype=np.int32)
     out = dict(c4_m=np.array(M), c4_n=np.array(N), c4_ks=np.array(KS, dtype=np.int32), c4_R=np.array(R),
+               c4_T=np.array(T), c4_R_total=np.array(R_TOTAL), c4_job_id=np.array(gids, dtype=np.int32),
                c4_seed=np.array(SEED), c4_A_sha256=np.array(a_sha), c4_job_k=job_k, c4_iters=iters,
                c4_labels_argmax=lam, c4_labels_rorder=lro, c4_margin_argmax=mam, c4_margin_rorder=mro)
     for k in KS:
-        sel = np.where(job_k == k)[0][:1]
+        sel = np.array(sorted(j for j in keep_jobs if job_k[j] == k))
         out[f"c4_H_k{k}"] = np.array([Hkeep[int(j)] for j in sel])
         out[f"c4_Hjobs_k{k}"] = sel.astype(np.int32)
     np.savez_compressed(OUT, **out)

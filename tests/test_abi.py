@@ -191,3 +191,34 @@ def test_solo_path_shape_limits():
     rc = L.nmfc_mu_solo(A.ctypes.data_as(dp), 1000, 41, 2, 10, 1, W.ctypes.data_as(dp), H.ctypes.data_as(dp),
                         W.ctypes.data_as(dp), H.ctypes.data_as(dp), ctypes.byref(it), ctypes.byref(early))
     assert rc == -1 and "bad arguments" in _lib.last_error()
+
+
+def test_generate_matrix_fills_despite_stale_errno(golden, monkeypatch):
+    """The reference's generateMatrix returns early, W/H unfilled, when errno is set on entry (generatematrix.c:86-90);
+    the drop-in fills them anyway, NMFC_GENERATE_ERRNO_COMPAT=1 restores the early return."""
+    import errno
+    from nmfconsensus_amd import _lib
+    L = ctypes.CDLL(os.path.join(ROOT, "nmfconsensus_amd", "lib", "libnmf.so"), use_errno=True)
+    libc = ctypes.CDLL(None)
+    libc.srand.argtypes = [ctypes.c_uint]
+    L.randnumber.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.randnumber.restype = ctypes.c_double
+    L.randnumber(0, 1)
+    dp = ctypes.POINTER(ctypes.c_double)
+    c = ctypes.c_int
+
+    def gen():
+        W = np.zeros((1000, 3), order="F")
+        H = np.zeros((3, 40), order="F")
+        libc.srand(123)
+        ctypes.set_errno(errno.EISDIR)
+        L.generateMatrix(ctypes.byref(c(1000)), ctypes.byref(c(40)), ctypes.byref(c(3)), ctypes.byref(c(0)),
+                         ctypes.byref(c(0)), ctypes.byref(c(1)), W.ctypes.data_as(dp), H.ctypes.data_as(dp), None, None)
+        return W, H
+
+    W, H = gen()
+    assert np.array_equal(W, golden["init_k3_W"]) and np.array_equal(H, golden["init_k3_H"])
+    monkeypatch.setenv("NMFC_GENERATE_ERRNO_COMPAT", "1")
+    W, H = gen()
+    assert not W.any() and not H.any()
+    assert _lib.lib() is not None

@@ -186,3 +186,55 @@ def test_restart_groups_split_and_merge(G):
     grp.close()
     with pytest.raises(ValueError):
         RestartGroups(np.zeros((10, 5)), groups=9, engine_cls=_FakeEngine)
+
+
+def _failing_worker(rank, world, port, timeout_s):
+    """Rank 1 dies before the counts all-reduce; rank 0 must leave the collective with an error (exit non-zero)
+    within the process group's timeout instead of blocking."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(world)
+    from nmfconsensus_amd.distributed import init_distributed, run_sharded_with
+    init_distributed("gloo", timeout_s=timeout_s)
+    if rank == 1:
+        raise SystemExit(3)   # a dead rank: no all-reduce, no destroy_process_group
+    run_sharded_with(lambda b, e: np.zeros((1, 4, 4), dtype=np.int32), [2], 4, 4, rank=rank, world=world)
+    sys.exit(0)   # not reached: the all-reduce raises
+
+
+@pytest.mark.timeout(200)
+def test_gloo_dead_rank_fails_fast():
+    import time
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    timeout_s = 20.0
+    ps = [ctx.Process(target=_failing_worker, args=(r, 2, port, timeout_s)) for r in range(2)]
+    t0 = time.time()
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=150)
+    elapsed = time.time() - t0
+    assert all(p.exitcode is not None for p in ps), "a rank is still blocked"
+    for p in ps:
+        if p.exitcode is None:
+            p.kill()
+    assert ps[1].exitcode == 3
+    assert ps[0].exitcode != 0, "the surviving rank reported success without its peer"
+    assert elapsed < timeout_s + 120, elapsed
+
+
+def test_init_distributed_timeout_default(monkeypatch):
+    import datetime
+    import torch.distributed as dist
+    from nmfconsensus_amd import distributed
+    seen = {}
+    monkeypatch.setattr(dist, "init_process_group", lambda backend, **kw: seen.update(backend=backend, **kw))
+    monkeypatch.delenv("NMFC_DIST_TIMEOUT_S", raising=False)
+    assert distributed.init_distributed("gloo") == distributed.DEFAULT_TIMEOUT_S
+    assert seen["timeout"] == datetime.timedelta(seconds=distributed.DEFAULT_TIMEOUT_S) and "device_id" not in seen
+    monkeypatch.setenv("NMFC_DIST_TIMEOUT_S", "42")
+    distributed.init_distributed("nccl", device="cuda:0")
+    assert seen["timeout"] == datetime.timedelta(seconds=42) and seen["device_id"] == "cuda:0"

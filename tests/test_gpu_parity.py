@@ -173,8 +173,11 @@ def test_nmf_mu_abi(golden):
 
 def test_nmf_mu_cache_follows_content(golden, monkeypatch):
     """The engine nmf_mu keeps across calls is reused only for the same A: A then A' (same shape, one entry
-    changed) then A again must each give what an uncached call gives (NMFC_NMF_MU_CACHE=0)."""
+    changed) then A again must each give what an uncached call gives (NMFC_NMF_MU_CACHE=0).  NMFC_SOLO=0 keeps
+    k = 3 off the solo kernel, so the engine path and its cache (compat.hip mu_cache_drop) are the ones tested."""
     from nmfconsensus_amd import _lib, libnmf
+    _lib.lib().nmfc_nmf_mu_release()
+    monkeypatch.setenv("NMFC_SOLO", "0")
     A = golden["A_gct"]
     A2 = A.copy(order="F")
     A2[517, 23] += 0.25
@@ -189,6 +192,7 @@ def test_nmf_mu_cache_follows_content(golden, monkeypatch):
     monkeypatch.delenv("NMFC_NMF_MU_CACHE")
     again = libnmf.nmf_mu(A, W0, H0, 40)   # a fresh engine after the release
     assert np.array_equal(again["h0"], fresh[0]["h0"])
+    _lib.lib().nmfc_nmf_mu_release()       # later tests get an engine made without NMFC_SOLO=0
 
 
 def test_nmf_mu_solo_cache_follows_content(golden):
@@ -377,18 +381,23 @@ def test_c1_runif_sweep_vs_reference(gct_engine, golden_c2, rule, key):
             assert relfro(r.H[j], g[f"c1r_H_k{k}"][q]) < TOL
 
 
-@pytest.mark.parametrize("rule,key,kernel", [(0, "argmax", "auto"), (1, "rorder", "auto"), (1, "rorder", "team")])
+@pytest.mark.parametrize("rule,key,kernel", [(0, "argmax", "auto"), (1, "rorder", "auto"), (1, "rorder", "team"),
+                                             (0, "argmax", "nosolo")])
 def test_c2_sweep_vs_reference(golden_c2, rule, key, kernel, monkeypatch):
     """BASELINE configs[1] (C2): synthetic 1000 x 40, k = 2..8, R = 100 (700 jobs) in one sweep against the
     reference's own nmf_mu run job by job: exits, labels, counts and consensus bit-exact; H within 1e-9.
-    kernel "auto" runs the one-workgroup-per-block kernel (every batch does); "team" forces the team kernel, whose
-    teams then run ~14 blocks one after another (tag and buffer continuity across blocks)."""
+    kernel "auto": rank 2..4 on the one-workgroup solo kernel (one restart per workgroup), rank 5..8 on the
+    one-workgroup-per-block kernel, concurrently; "nosolo" (NMFC_SOLO=0) every rank on the block kernel; "team"
+    forces the team kernel for the blocks, whose teams then run ~10 blocks one after another (tag and buffer
+    continuity across blocks)."""
     from nmfconsensus_amd.nmf import Engine
     g = golden_c2
     ks = [int(k) for k in g["c2_ks"]]
     R = int(g["c2_R"])
-    if kernel != "auto":
+    if kernel == "team":
         monkeypatch.setenv("NMFC_SMALL_KERNEL", kernel)
+    elif kernel == "nosolo":
+        monkeypatch.setenv("NMFC_SOLO", "0")
     with Engine(g["c2_A"]) as eng:
         r = eng.run(ks, R, maxiter=10000, seed=int(g["c2_seed"]), stop_rule=1, label_rule=rule, want_factors=True)
     assert np.array_equal(r.iters, g["c2_iters"])
@@ -448,6 +457,39 @@ def test_block_packed_tail_bit_identical():
     assert len(set(a.iters.tolist())) > 3   # restarts stop at different iterations: the tail is repacked
     for j in range(20):
         assert np.array_equal(a.W[j], b.W[j]) and np.array_equal(a.H[j], b.H[j]), j
+
+
+@pytest.mark.parametrize("ks,R", [([2, 3, 4, 5], 5), ([4, 2], 3)])
+def test_solo_batch_bitidentical_to_drop_in(golden, oracle, ks, R):
+    """A sweep's rank 2..4 restarts run on the solo kernel, one workgroup each (batched launches beside k_small_mu):
+    every such job's W/H, exit and labels are bit-identical to the same job through the single-restart drop-in
+    (nmfc_mu_solo with the job's own generateMatrix(ran) init), so a job's bits do not depend on the batch.  The gct
+    has n = 40, so k = 3 runs padded to the 4-row kernel (its zero row never mixes in)."""
+    import ctypes
+    from nmfconsensus_amd import _lib
+    from nmfconsensus_amd.nmf import Engine
+    A = golden["A_gct"]
+    m, n = A.shape
+    seed = 123
+    with Engine(A) as eng:
+        r = eng.run(ks, R, maxiter=10000, seed=seed, stop_rule=1, want_factors=True)
+    L = _lib.lib()
+    dp = ctypes.POINTER(ctypes.c_double)
+    checked = 0
+    for j in range(len(ks) * R):
+        k = ks[j % len(ks)]
+        if not L.nmfc_mu_solo_fits(m, n, k):
+            continue
+        W0, H0 = oracle.init_restart(seed + j, m, n, k)
+        W, H = np.zeros_like(W0, order="F"), np.zeros_like(H0, order="F")
+        it, early = ctypes.c_int(0), ctypes.c_int(0)
+        rc = L.nmfc_mu_solo(A.ctypes.data_as(dp), m, n, k, 10000, 1, W0.ctypes.data_as(dp), H0.ctypes.data_as(dp),
+                            W.ctypes.data_as(dp), H.ctypes.data_as(dp), ctypes.byref(it), ctypes.byref(early))
+        assert rc == 0, _lib.last_error()
+        assert r.iters[j] == it.value, (j, k)
+        assert np.array_equal(r.W[j], W) and np.array_equal(r.H[j], H), (j, k)
+        checked += 1
+    assert checked == sum(1 for j in range(len(ks) * R) if ks[j % len(ks)] <= 4)
 
 
 def test_small_path_agrees_with_batched_engine(golden):
@@ -542,12 +584,17 @@ def test_nmf_mu_abi_rank_above_16(golden):
 
 def test_nmf_mu_team_failure_falls_back(golden, monkeypatch):
     """A drop-in call whose team cannot meet (e.g. many processes sharing the GPU) runs on the batched engine
-    instead: the same exit and W/H to rounding (NMFC_TEAM_FAIL simulates the failure)."""
-    from nmfconsensus_amd import libnmf
+    instead: the same exit and W/H to rounding (NMFC_TEAM_FAIL simulates the failure).  NMFC_SOLO=0 (set before
+    the cached engine is made) keeps k = 3 on the gct off the solo kernel in both the drop-in and the fallback, so
+    the team and then k_small_mu run."""
+    from nmfconsensus_amd import _lib, libnmf
+    _lib.lib().nmfc_nmf_mu_release()
+    monkeypatch.setenv("NMFC_SOLO", "0")
     A, W0, H0 = golden["A_gct"], golden["init_k3_W"], golden["init_k3_H"]
     team = libnmf.nmf_mu(A, W0, H0, 10000)
     monkeypatch.setenv("NMFC_TEAM_FAIL", "1")
     fb = libnmf.nmf_mu(A, W0, H0, 10000)
+    _lib.lib().nmfc_nmf_mu_release()   # later tests get an engine made without NMFC_SOLO=0
     assert team["ret"] == 0 and fb["ret"] == 0
     assert fb["maxiter"] == team["maxiter"] == int(golden["refc_k3_iter"])
     assert relfro(fb["w0"], team["w0"]) < 1e-11 and relfro(fb["h0"], team["h0"]) < 1e-11

@@ -1,11 +1,12 @@
 """The oracle (our C restatement, oracle/nmf_oracle.c) pinned against the reference's golden vectors
 (tests/golden/golden.npz, produced by the reference's own C code) and against libc itself."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
 
-from conftest import relfro
+from conftest import ROOT, relfro
 
 TOL = 1e-9
 
@@ -129,3 +130,28 @@ def test_c2_and_runif_sweeps_subset(golden, golden_c2, oracle, tag):
             assert np.array_equal(oracle.labels(H, 0), g[f"{tag}_labels_argmax"][j])
             assert np.array_equal(oracle.labels(H, 1), g[f"{tag}_labels_rorder"][j])
             assert relfro(H, g[f"{tag}_H_k{k}"][q]) < TOL
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libnmf_ref.so")),
+                    reason="oracle/_ref not built (needs /root/reference)")
+def test_reflib_generate_ran_is_errno_safe(golden):
+    """The reference's generateMatrix returns early, W/H untouched, whenever errno is set on entry
+    (generatematrix.c:86-90, ERROR_CHECKING at common.h:25).  RefLib.generate_ran clears errno first, so a
+    stale EISDIR from an earlier call still gives the golden init; the raw call with errno set shows the
+    early return (and generate_ran would raise on an unfilled W/H)."""
+    import ctypes
+    import errno
+    from pyoracle import RefLib, _d
+    ref = RefLib()
+    ctypes.set_errno(errno.EISDIR)
+    W, H = ref.generate_ran(123, 1000, 40, 3)
+    assert np.array_equal(W, golden["init_k3_W"]) and np.array_equal(H, golden["init_k3_H"])
+    # the reference's own behaviour, called raw with errno set on entry: nothing is written
+    ref.seed(123)
+    W2 = np.zeros((1000, 3), order="F")
+    H2 = np.zeros((3, 40), order="F")
+    c = ctypes.c_int
+    ctypes.set_errno(errno.EISDIR)
+    ref.L.generateMatrix(ctypes.byref(c(1000)), ctypes.byref(c(40)), ctypes.byref(c(3)), ctypes.byref(c(0)),
+                         ctypes.byref(c(0)), ctypes.byref(c(1)), _d(W2), _d(H2), None, None)
+    assert not W2.any() and not H2.any()
