@@ -148,3 +148,39 @@ def test_bad_arguments():
             eng.run([17], 1)
         with pytest.raises(RuntimeError):
             eng.run([2], 1, stopfreq=0)
+
+
+def test_c5_full_size_stop_rule_vs_oracle():
+    """BASELINE configs[4] at full size under the real NMF.div stop rule (tests/golden/golden_c5.npz, made by
+    tests/golden/make_golden_c5.py from the Brunet oracle): 20000 x 500, k = 2..10, one restart per k
+    (set.seed(rseed + 1)), stopconv 40 / stopfreq 10, maxniter 2000.  Iterations, labels and counts bit-exact;
+    H within 1e-9; W within 1e-9 on its first W_ROWS rows for every k and on the whole of k = 10."""
+    import hashlib
+    import os
+    from conftest import ROOT
+    from nmfconsensus_amd.brunet import BrunetEngine
+    from nmfconsensus_amd.synthetic import planted_matrix
+    path = os.path.join(ROOT, "tests", "golden", "golden_c5.npz")
+    if not os.path.exists(path):
+        pytest.skip("golden_c5.npz not generated")
+    with np.load(path, allow_pickle=False) as z:
+        g = {k: z[k] for k in z.files}
+    A = planted_matrix(int(g["c5_m"]), int(g["c5_n"]))
+    assert hashlib.sha256(np.ascontiguousarray(A).tobytes(order="F")).hexdigest() == str(g["c5_A_sha256"])
+    ks = [int(k) for k in g["c5_ks"]]
+    n = A.shape[1]
+    with BrunetEngine(A) as eng:
+        r = eng.run(ks, 1, maxiter=int(g["c5_maxiter"]), seed=int(g["c5_rseed"]), stopconv=int(g["c5_stopconv"]),
+                    stopfreq=int(g["c5_stopfreq"]), want_factors=True)
+    assert np.array_equal(r.iters, g["c5_iters"]), (r.iters, g["c5_iters"])
+    assert np.array_equal(r.labels, g["c5_labels_argmax"].astype(np.int32))
+    rows = int(g["c5_W_rows"])
+    for i, k in enumerate(ks):
+        assert relfro(r.H[i], g[f"c5_H_k{k}"]) < TOL, k
+        assert relfro(r.W[i][:rows], g[f"c5_Wtop_k{k}"]) < TOL, k
+        lab = g["c5_labels_argmax"][i].astype(np.int32)
+        assert np.array_equal(r.counts[i], (lab[:, None] == lab[None, :]).astype(np.int32)), k
+        assert np.array_equal(r.consensus[i], r.counts[i] / 1.0)
+    kf = int(g["c5_W_full_k"])
+    assert relfro(r.W[ks.index(kf)], g["c5_W_full"]) < TOL
+    assert r.counts.shape == (len(ks), n, n)

@@ -35,6 +35,7 @@ for s, e, nm, g in rows:
     sp[0] = s if sp[0] is None else sp[0]
     sp[1] = e
 useful = None
+live = {}
 if len(sys.argv) > 3:
     import numpy as np
     kk, its = np.load(sys.argv[3])
@@ -42,9 +43,13 @@ if len(sys.argv) > 3:
     nn = int(sys.argv[5]) if len(sys.argv) > 5 else 500
     F = 4.0 * mm * nn * kk + 4.0 * (mm + nn) * kk * kk
     useful = {}
+    live = {}
     for b in agg:
         lo, hi = b * bucket, (b + 1) * bucket
         useful[b] = float(np.sum(F * np.clip(its - lo, 0, hi - lo)))
+        # mean live restarts / live columns over the bucket's iterations
+        live[b] = (float(np.sum(np.clip(its - lo, 0, hi - lo))) / bucket,
+                   float(np.sum(kk * np.clip(its - lo, 0, hi - lo))) / bucket)
 tot = 0.0
 print(f"{'iters':>11s} {'span ms':>8s} {'gap ms':>7s} {'TF':>6s}  kernels (ms, mean grid)")
 for b in sorted(agg):
@@ -52,7 +57,8 @@ for b in sorted(agg):
     tot += sp
     parts = "  ".join(f"{k}={v:.1f}({sum(grids[b][k]) / len(grids[b][k]):.0f})" for k, v in sorted(agg[b].items()) if v > 0.05)
     tf = useful[b] / (sp * 1e-3) / 1e12 if useful else float("nan")
-    print(f"{b * bucket:5d}-{(b + 1) * bucket:5d} {sp:8.1f} {gap[b]:7.2f} {tf:6.1f}  {parts}")
+    lv = f" live {live[b][0]:6.1f} r {live[b][1]:7.1f} c" if useful else ""
+    print(f"{b * bucket:5d}-{(b + 1) * bucket:5d} {sp:8.1f} {gap[b]:7.2f} {tf:6.1f}{lv}  {parts}")
 print(f"total span {tot:.1f} ms over {it} iterations")
 gaps = sorted(((rows[i + 1][0] - rows[i][1], i) for i in range(len(rows) - 1)), reverse=True)
 print("largest idle gaps:")
