@@ -28,6 +28,17 @@ sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix peak (spec); probe measured ~70
 HBM_PEAK_GBS = 8000.0
+# fp64 VALU issue: 78.6 TF = 1024 SIMDs x 2.4 GHz x 16 fp64 FMA lanes per cycle (a wave64 v_fma_f64 every 4 cycles);
+# in lane-instructions per second that is 39.3 T (each FMA, add, mul or divide step counts one)
+FP64_VALU_PEAK_TOPS = FP64_MFMA_PEAK_TFLOPS / 2
+# Brunet: VALU lane-instructions per matrix element and iteration, per side (H update, W update), as compiled
+# (csrc/brunet.hip, tools ISA listing): k FMAs of VP = W H, the divide q = a / VP (v_rcp_f64 + two Newton steps
+# (4 FMA) + mul + residual FMA + correction FMA = 8), k FMAs accumulating W^T Q or Q H^T
+BRUNET_DIV_OPS = 8
+
+
+def brunet_valu_ops_per_element(k: int) -> int:
+    return 2 * (2 * k + BRUNET_DIV_OPS)
 
 
 def log(*a):
@@ -742,7 +753,8 @@ def bench_brunet(args, rank, world, local, dev):
         # per-launch events there overlap.  The kernels' own rates come from a serialized pass (one
         # lane) over the same matrix: every k, R restarts, 40 fixed iterations, HIP events per launch.
         eng.set_timing(True)
-        kacc = {kid: [0, 0.0, 0.0] for kid in (_lib.BK_HNUM, _lib.BK_HUPD, _lib.BK_WUPD)}
+        # per kernel: [launches, ms, rank-k flop x launches, VALU lane-instructions x launches]
+        kacc = {kid: [0, 0.0, 0.0, 0.0] for kid in (_lib.BK_HNUM, _lib.BK_HUPD, _lib.BK_WUPD)}
         for k in ks:
             eng.run([k], R, maxiter=40, stopconv=10 ** 6, want_counts=False, lanes=1)
             for kid, a in kacc.items():
@@ -750,21 +762,34 @@ def bench_brunet(args, rank, world, local, dev):
                 a[0] += c
                 a[1] += ms
                 a[2] += fl * c
+                # rank-k flop per launch = 4 m n k per restart (one side): elements x (2k + DIV) VALU ops
+                a[3] += fl * c / (4.0 * k) * (2 * k + BRUNET_DIV_OPS)
         kernels = {}
         for name, kid in (("hnum", _lib.BK_HNUM), ("hupd", _lib.BK_HUPD), ("wupd", _lib.BK_WUPD)):
-            c, ms, fl = kacc[kid]
+            c, ms, fl, ops = kacc[kid]
             kernels[name] = {"launches": c, "avg_ms": ms / max(c, 1)}
             if fl:
                 kernels[name]["algo_flop_per_launch"] = fl / c
                 kernels[name]["tflops"] = fl / c / (ms / c * 1e-3) / 1e12
+                kernels[name]["valu_ops_per_launch"] = ops / c
+                kernels[name]["valu_tops"] = ops / c / (ms / c * 1e-3) / 1e12
+                kernels[name]["frac_valu"] = kernels[name]["valu_tops"] / FP64_VALU_PEAK_TOPS
         dom = max(("hnum", "wupd"), key=lambda s: kernels[s]["avg_ms"] * kernels[s]["launches"])
-        ach = kernels[dom]["tflops"]
-        roof = {"bound": "valu", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None, "kernels": kernels,
+        ach = kernels[dom]["valu_tops"]
+        sweep_ops = float(np.sum(m * n * np.array([brunet_valu_ops_per_element(int(k)) for k in ks_job]) * res.iters)) * world
+        roof = {"bound": "valu", "kernel": dom, "achieved": ach, "peak": FP64_VALU_PEAK_TOPS,
+                "unit": "T fp64 VALU lane-instructions/s", "frac": ach / FP64_VALU_PEAK_TOPS, "traffic": None,
+                "kernels": kernels,
+                "rank_k_tflops": kernels[dom]["tflops"], "rank_k_frac_of_78.6TF": kernels[dom]["tflops"] / FP64_MFMA_PEAK_TFLOPS,
+                "sweep_valu_tops": sweep_ops / (elapsed / args.steps) / 1e12,
                 "sweep_tflops": sweep_flop / (elapsed / args.steps) / 1e12,
-                "note": "fp64 VALU (FMA + divide); peak = the 78.6 TF fp64 vector spec; flops count only the "
-                        "rank-k products (4 m n k per restart and kernel), not the m n divides; kernel rates from a "
-                        "serialized 40-iteration pass per k (R restarts), sweep_tflops = whole timed sweep"}
+                "valu_ops_per_element_iteration": {str(k): brunet_valu_ops_per_element(k) for k in ks},
+                "note": "fp64 VALU issue roofline: per matrix element and iteration 2 x (2k FMA + the compiled divide, "
+                        f"{BRUNET_DIV_OPS} VALU instructions: rcp + 2 Newton steps + mul + residual + correction), peak "
+                        "= 1024 SIMDs x 2.4 GHz x 16 fp64 lanes per cycle = 39.3 T lane-instructions/s (the 78.6 TF "
+                        "fp64 vector spec / 2); v_rcp_f64 is counted as one slot and address arithmetic not at all, so "
+                        "the fraction is a lower bound on VALU issue use; kernel rates from a serialized 40-iteration "
+                        "pass per k (R restarts); rank_k_tflops counts the 8 m n k product flops alone"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -36,7 +37,7 @@ __all__ = [
     "Engine", "SweepResult", "doNMF", "createJobArray", "runNMFinJobs", "computeConsensusMatrixFromClusterings",
     "computeConsensusAndSaveFiles", "cophenetic", "cophenetic_batch", "cutree", "job_grid",
     "STOP_FIXED", "STOP_REF_COMPAT", "STOP_ARGMAX_STABLE", "STOP_TOLX", "LABEL_ARGMAX", "LABEL_R_ORDER",
-    "INIT_LIBNMF", "INIT_R_RUNIF",
+    "INIT_LIBNMF", "INIT_R_RUNIF", "release_doNMF_engine",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -233,13 +234,45 @@ class Engine:
                            max_iter_run=res.max_iter_run, job_begin=jb, job_end=je)
 
 
+_DONMF = {"A": None, "eng": None, "device": None}
+_DONMF_LOCK = threading.Lock()
+
+
+def _donmf_engine(A: np.ndarray, device: int) -> "Engine":
+    """The Engine doNMF reuses across calls (nmf.r calls doNMF once per restart on one matrix): kept while A is
+    byte-identical to the cached host copy and the device is the same; anything else builds a new one."""
+    c = _DONMF
+    if c["eng"] is not None and c["device"] == device and c["A"].shape == A.shape and np.array_equal(c["A"], A):
+        return c["eng"]
+    release_doNMF_engine_locked()
+    c["eng"] = Engine(A, device)
+    c["A"], c["device"] = A.copy(order="F"), device
+    return c["eng"]
+
+
+def release_doNMF_engine_locked():
+    c = _DONMF
+    if c["eng"] is not None:
+        c["eng"].close()
+    c["eng"] = c["A"] = c["device"] = None
+
+
+def release_doNMF_engine():
+    """Frees the engine (HBM, A's layouts) that doNMF keeps between calls."""
+    with _DONMF_LOCK:
+        release_doNMF_engine_locked()
+
+
 def doNMF(A, k: int, maxniter: int, seed: int = 123, tolerance: float = 1e-4, num_clusterings=None,
-          *, job_id: int = 1, stop_rule: int = STOP_REF_COMPAT, init_stream: int = INIT_LIBNMF):
+          *, job_id: int = 1, stop_rule: int = STOP_REF_COMPAT, init_stream: int = INIT_LIBNMF, device: int = -1):
     """nmf.r:23-51 -- one restart: init W, H (generateMatrix(ran) stream, seed + job_id - 1), run the
     MU loop on the GPU, return dict(W=m x k, H=k x n, iter=iterations).  `tolerance` is accepted and
-    unused, like the reference (nmf_mu.c:92-93)."""
+    unused, like the reference (nmf_mu.c:92-93).  The engine (A resident in HBM in its layouts) is kept for
+    the next call with the same A (release_doNMF_engine() frees it)."""
     del tolerance, num_clusterings
-    with Engine(A) as eng:
+    A = _f64(A)
+    with _DONMF_LOCK:
+        eng = _donmf_engine(A, device)
         # a single-job "grid" whose job seed is seed + job_id - 1
         r = eng.run([k], 1, maxiter=maxniter, seed=seed + job_id - 1, stop_rule=stop_rule, want_factors=True,
                     want_counts=False, init_stream=init_stream)

@@ -33,11 +33,23 @@ def test_runNMFinJobs_rejects_k1(golden):
 
 
 def test_doNMF(golden):
+    from nmfconsensus_amd import nmf
     from nmfconsensus_amd.nmf import doNMF
     r = doNMF(golden["A_gct"], 3, 10, seed=123)
     assert r["iter"] == 10
     assert relfro(r["W"], golden["fixed_k3_T10_W"]) < 1e-9
     assert relfro(r["H"], golden["fixed_k3_T10_H"]) < 1e-9
+    # the engine is kept for the next call on the same matrix and rebuilt for another one
+    eng = nmf._DONMF["eng"]
+    r2 = doNMF(np.array(golden["A_gct"]), 3, 10, seed=123)
+    assert nmf._DONMF["eng"] is eng
+    assert np.array_equal(r2["W"], r["W"]) and np.array_equal(r2["H"], r["H"])
+    A2 = golden["A_gct"].copy(order="F")
+    A2[5, 5] += 1.0
+    r3 = doNMF(A2, 3, 10, seed=123)
+    assert nmf._DONMF["eng"] is not eng and not np.array_equal(r3["H"], r["H"])
+    nmf.release_doNMF_engine()
+    assert nmf._DONMF["eng"] is None
 
 
 def test_counts_into_device_tensor(golden):
