@@ -468,7 +468,7 @@ def test_solo_batch_bitidentical_to_drop_in(golden, oracle, ks, R):
     import ctypes
     from nmfconsensus_amd import _lib
     from nmfconsensus_amd.nmf import Engine
-    A = golden["A_gct"]
+    A = np.asfortranarray(golden["A_gct"])   # the C ABI takes column-major A
     m, n = A.shape
     seed = 123
     with Engine(A) as eng:

@@ -60,6 +60,17 @@ for b in sorted(agg):
     lv = f" live {live[b][0]:6.1f} r {live[b][1]:7.1f} c" if useful else ""
     print(f"{b * bucket:5d}-{(b + 1) * bucket:5d} {sp:8.1f} {gap[b]:7.2f} {tf:6.1f}{lv}  {parts}")
 print(f"total span {tot:.1f} ms over {it} iterations")
+# idle time by the kernel that FOLLOWS the gap (boundary gaps before each MU kernel, poll copies, repack moves)
+by_next = collections.defaultdict(lambda: [0.0, 0])
+for i in range(len(rows) - 1):
+    g = rows[i + 1][0] - rows[i][1]
+    if g > 0:
+        nm = rows[i + 1][2].split("<")[0]
+        by_next[nm][0] += g / 1e6
+        by_next[nm][1] += 1
+print("idle before each kernel kind (ms total, count, us mean):")
+for nm, (ms, c) in sorted(by_next.items(), key=lambda x: -x[1][0])[:10]:
+    print(f"  {nm[:40]:40s} {ms:8.2f} {c:7d} {ms / c * 1e3:8.1f}")
 gaps = sorted(((rows[i + 1][0] - rows[i][1], i) for i in range(len(rows) - 1)), reverse=True)
 print("largest idle gaps:")
 for g, i in gaps[:8]:
