@@ -308,18 +308,7 @@ struct nmfc_engine {
   DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp, smallblk;
   DevBuf teamG, teamSW, teamFlag;   // k_team_mu: partial buffers, per-workgroup flags (+ the error word)
   DevBuf solojobs;                  // batched k_solo_mu jobs (small shapes, rank <= 4)
-  // stream-ordered repacks (env NMFC_ASYNC_REPACK=0: the draining form): a pinned stop_iter snapshot taken behind
-  // the enqueued chunks, and two pinned staging slots for a repack's uploads (a slot is refilled only after the
-  // stream has consumed the repack that last used it)
-  bool async_repack = true;
-  int* h_si = nullptr;
-  size_t h_si_n = 0;
-  hipEvent_t snap_ev = nullptr;
-  char* stage[2] = {nullptr, nullptr};
-  size_t stage_cap[2] = {0, 0};
-  hipEvent_t stage_ev[2] = {nullptr, nullptr};
-  bool stage_used[2] = {false, false};
-  int stage_slot = 0;
+  bool hupd_latency = true;         // env NMFC_HUPD_LATENCY=0: always the full-load k_hupdate form
   bool solo_ok = true;              // env NMFC_SOLO=0: no solo kernel (every small-shape restart in k_small_mu blocks)
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // the solo launches (one per kernel rank) beside k_small_mu
   hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
@@ -353,33 +342,6 @@ struct nmfc_engine {
 };
 
 namespace {
-
-// A pinned staging slot of at least `bytes` for one repack's uploads: the other slot than the last repack's, waited
-// for until the stream has consumed the uploads that last filled it.  nullptr on failure (error set).
-char* stage_begin(nmfc_engine* e, size_t bytes) {
-  const int sl = e->stage_slot ^= 1;
-  if (e->stage_used[sl] && hipEventSynchronize(e->stage_ev[sl]) != hipSuccess) {
-    set_err("stage_begin: event synchronize failed");
-    return nullptr;
-  }
-  e->stage_used[sl] = false;
-  if (!e->stage_ev[sl] && hipEventCreateWithFlags(&e->stage_ev[sl], hipEventDisableTiming) != hipSuccess) {
-    set_err("stage_begin: hipEventCreate failed");
-    return nullptr;
-  }
-  if (e->stage_cap[sl] < bytes) {
-    if (e->stage[sl]) (void)hipHostFree(e->stage[sl]);
-    e->stage[sl] = nullptr;
-    e->stage_cap[sl] = 0;
-    const size_t cap = std::max<size_t>(bytes, 1 << 16);
-    if (hipHostMalloc((void**)&e->stage[sl], cap, 0) != hipSuccess) {
-      set_err("stage_begin: hipHostMalloc(%zu) failed", cap);
-      return nullptr;
-    }
-    e->stage_cap[sl] = cap;
-  }
-  return e->stage[sl];
-}
 
 // Tile shapes for one chunk of iterations, from a wave-quantised cost model: a shape's time is
 // ceil(workgroups / resident slots) x its relative per-workgroup time.  Slots per CU and relative
@@ -633,7 +595,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_NARROW_MAXB")) e->narrow_maxb = std::min(8, std::max(1, atoi(s)));
   if (const char* s = getenv("NMFC_SMALL")) e->small_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SOLO")) e->solo_ok = atoi(s) != 0;
-  if (const char* s = getenv("NMFC_ASYNC_REPACK")) e->async_repack = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_HUPD_LATENCY")) e->hupd_latency = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SMALL_KERNEL"))
     e->small_kernel = std::string(s) == "team" ? 1 : std::string(s) == "single" ? 2 : 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
@@ -705,12 +667,6 @@ void nmfc_engine_destroy(nmfc_engine* e) {
                     &e->teamFlag,  &e->mu1_dev,   &e->mu1_G,     &e->mu1_SW,    &e->mu1_flag};
   for (DevBuf* b : bufs) b->release();
   e->solojobs.release();
-  if (e->h_si) (void)hipHostFree(e->h_si);
-  if (e->snap_ev) (void)hipEventDestroy(e->snap_ev);
-  for (int q = 0; q < 2; ++q) {
-    if (e->stage[q]) (void)hipHostFree(e->stage[q]);
-    if (e->stage_ev[q]) (void)hipEventDestroy(e->stage_ev[q]);
-  }
   for (int q = 0; q < 3; ++q) {
     if (e->aux[q]) (void)hipStreamDestroy(e->aux[q]);
     if (e->join_ev[q]) (void)hipEventDestroy(e->join_ev[q]);
@@ -1038,17 +994,6 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   HCHECK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
   HCHECK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
   std::vector<int> si(nj);
-  bool snap_pending = false;
-  if (!small && e->async_repack) {
-    if (e->h_si_n < (size_t)nj) {
-      if (e->h_si) (void)hipHostFree(e->h_si);
-      e->h_si = nullptr;
-      e->h_si_n = 0;
-      HCHECK(hipHostMalloc((void**)&e->h_si, sizeof(int) * nj, 0));
-      e->h_si_n = nj;
-    }
-    if (!e->snap_ev) HCHECK(hipEventCreateWithFlags(&e->snap_ev, hipEventDisableTiming));
-  }
   for (; !small;) {
     if (it < opts.maxiter) {
       const int chunk = std::min(opts.check_every, opts.maxiter - it);
@@ -1115,7 +1060,9 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         }
         {
           TimedLaunch tl(e, KID_HUPD, iter % e->timing_stride == 0);
-          hipLaunchKernelGGL(k_hupdate, dim3(nact), dim3(NTH), 0, st, iter, opts.maxiter, opts.stop_rule,
+          // one workgroup per live restart: the latency form when each has a CU of its own (same bits)
+          auto kh = (nact <= e->ncu && e->hupd_latency) ? k_hupdate<100, 2> : k_hupdate<32, 4>;
+          hipLaunchKernelGGL(kh, dim3(nact), dim3(NTH), 0, st, iter, opts.maxiter, opts.stop_rule,
                              e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, e->nsplit,
                              e->SWpart.as<double>(), sw_total, e->H[cur].as<double>(), e->SH.as<double>(),
                              e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->unchanged.as<int>(),
@@ -1169,101 +1116,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     }
     if (e->timing) drain_timing(e);
     if (done || (it >= opts.maxiter && checked == q)) break;
-    const bool repack_due = stopped - stopped_at_pack >= std::max(1, nact / e->repack_div);
-    if (e->async_repack) {
-      // Stream-ordered repack: when due, a snapshot of stop_iter is copied behind the chunks already enqueued; the
-      // next chunk is enqueued with the current packing (the restarts stopped since sit in it as dead columns for
-      // those iterations), and once the snapshot has landed -- behind that chunk's predecessor, so the GPU is still
-      // busy with it -- the archive of the stopped restarts, the moves and the new packing are enqueued from pinned
-      // staging behind it.  The stream never drains for a repack.
-      if (snap_pending) {
-        snap_pending = false;
-        if (it >= opts.maxiter) continue;   // nothing left to enqueue with a new packing
-        HCHECK(hipEventSynchronize(e->snap_ev));
-        std::vector<RestartInfo> gone, live;
-        for (const RestartInfo& r : pk.ri) {
-          if (!e->h_si[r.rid])
-            live.push_back(r);
-          else if (!archived[r.rid])
-            gone.push_back(r);
-        }
-        Packing np = pack(live);
-        const bool fits = (long)np.npanels * PANEL <= cap_cols;   // see the draining form below
-        const size_t nmv = gone.size() + (fits ? np.ri.size() : 0);
-        const size_t bytes = sizeof(MoveJob) * (nmv + 2) + (fits ? sizeof(RestartInfo) * (np.ri.size() + 1) +
-                                                                      sizeof(int) * 2 * np.npanels +
-                                                                      sizeof(ColInfo) * np.ci.size()
-                                                                : 0) + 256;
-        char* sb = stage_begin(e, bytes);
-        if (!sb) return -1;
-        size_t off = 0;
-        auto take = [&](size_t b) {
-          char* p = sb + off;
-          off += (b + 63) / 64 * 64;
-          return p;
-        };
-        MoveJob* mvg = reinterpret_cast<MoveJob*>(take(sizeof(MoveJob) * (gone.size() + 1)));
-        MoveJob* mvm = reinterpret_cast<MoveJob*>(take(sizeof(MoveJob) * (nmv - gone.size() + 1)));
-        // archive: final H (and W) of the stopped restarts out of the current buffers (their rows no longer change)
-        if (!gone.empty()) {
-          for (size_t x = 0; x < gone.size(); ++x) mvg[x] = {gone[x].col0, hoff[gone[x].rid], gone[x].k};
-          HCHECK(hipMemcpyAsync(e->moves.p, mvg, sizeof(MoveJob) * gone.size(), hipMemcpyHostToDevice, st));
-          {
-            TimedLaunch tl(e, KID_OTHER);
-            hipLaunchKernelGGL(k_move_rows, dim3((unsigned)gone.size(), 2), dim3(NT), 0, st, e->moves.as<MoveJob>(),
-                               e->H[cur].as<double>(), e->n_pad, e->Hfin.as<double>(), e->n_pad, e->n_pad);
-            if (want_w)
-              hipLaunchKernelGGL(k_move_rows, dim3((unsigned)gone.size(), 16), dim3(NT), 0, st, e->moves.as<MoveJob>(),
-                                 e->W[cur].as<double>(), e->m_pad, e->Wfin.as<double>(), e->m_pad, e->m_pad);
-          }
-          HCHECK(hipGetLastError());
-          for (const RestartInfo& r : gone) archived[r.rid] = 1;
-        }
-        if (fits) {
-          std::vector<int> old_col(nj, -1);
-          for (const RestartInfo& r : live) old_col[r.rid] = r.col0;
-          for (size_t x = 0; x < np.ri.size(); ++x) mvm[x] = {old_col[np.ri[x].rid], np.ri[x].col0, np.ri[x].k};
-          MoveJob* dmv = e->moves.as<MoveJob>() + gone.size();   // behind the archive's jobs: no overwrite race
-          if (!np.ri.empty()) {
-            HCHECK(hipMemcpyAsync(dmv, mvm, sizeof(MoveJob) * np.ri.size(), hipMemcpyHostToDevice, st));
-            TimedLaunch tl(e, KID_OTHER);
-            hipLaunchKernelGGL(k_move_rows, dim3((unsigned)np.ri.size(), 16), dim3(NT), 0, st, dmv, e->W[cur].as<double>(),
-                               e->m_pad, e->W[cur ^ 1].as<double>(), e->m_pad, e->m_pad);
-            hipLaunchKernelGGL(k_move_rows, dim3((unsigned)np.ri.size(), 2), dim3(NT), 0, st, dmv, e->H[cur].as<double>(),
-                               e->n_pad, e->H[cur ^ 1].as<double>(), e->n_pad, e->n_pad);
-          }
-          HCHECK(hipGetLastError());
-          RestartInfo* sri = reinterpret_cast<RestartInfo*>(take(sizeof(RestartInfo) * (np.ri.size() + 1)));
-          int* sprb = reinterpret_cast<int*>(take(sizeof(int) * np.npanels));
-          int* spre = reinterpret_cast<int*>(take(sizeof(int) * np.npanels));
-          ColInfo* sci = reinterpret_cast<ColInfo*>(take(sizeof(ColInfo) * np.ci.size()));
-          if (!np.ri.empty()) memcpy(sri, np.ri.data(), sizeof(RestartInfo) * np.ri.size());
-          memcpy(sprb, np.prb.data(), sizeof(int) * np.npanels);
-          memcpy(spre, np.pre.data(), sizeof(int) * np.npanels);
-          memcpy(sci, np.ci.data(), sizeof(ColInfo) * np.ci.size());
-          HCHECK(hipMemcpyAsync(e->rinfo.p, sri, sizeof(RestartInfo) * std::max<size_t>(np.ri.size(), 1),
-                                hipMemcpyHostToDevice, st));
-          HCHECK(hipMemcpyAsync(e->prb.p, sprb, sizeof(int) * np.npanels, hipMemcpyHostToDevice, st));
-          HCHECK(hipMemcpyAsync(e->pre.p, spre, sizeof(int) * np.npanels, hipMemcpyHostToDevice, st));
-          HCHECK(hipMemcpyAsync(e->colinfo.p, sci, sizeof(ColInfo) * np.ci.size(), hipMemcpyHostToDevice, st));
-          cur ^= 1;
-          pk = np;
-          nact = (int)pk.ri.size();
-          ++e->repacks;
-        }
-        HCHECK(hipEventRecord(e->stage_ev[e->stage_slot], st));
-        e->stage_used[e->stage_slot] = true;
-        stopped_at_pack = nj - (int)live.size();
-        if (fits && nact == 0) break;
-      } else if (repack_due) {
-        HCHECK(hipMemcpyAsync(e->h_si, e->stop_iter.p, sizeof(int) * nj, hipMemcpyDeviceToHost, st));
-        HCHECK(hipEventRecord(e->snap_ev, st));
-        snap_pending = true;
-      }
-      continue;
-    }
-    // draining form: repack when a fraction 1/repack_div of the live restarts have stopped since the last packing
-    if (repack_due) {
+    // repack when a fraction 1/repack_div of the live restarts have stopped since the last packing
+    if (stopped - stopped_at_pack >= std::max(1, nact / e->repack_div)) {
       HCHECK(hipStreamSynchronize(st));
       if (e->timing) drain_timing(e);
       checked = q;   // every poll is now complete

@@ -643,7 +643,7 @@ struct HupdSmem {
 // partials of one sample are loaded GS chunks at a time (GS*K <= 64 values in flight per thread).  The
 // arithmetic order is fixed: chunk partials and Gram partials summed in chunk order, d = sum_b in b order,
 // h h^T by T = f(k) threads per pair over j = pq (mod T) in j order, then the T partials in pq order.
-template <int K>
+template <int K, int GSV = 32>
 __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int maxiter, int stop_rule, int n,
                                              long n_pad, const double* __restrict__ Gpart, long g_ld, long g_split,
                                              int nsplit, const double* __restrict__ SWpart, long sw_total,
@@ -652,10 +652,9 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
                                              int* __restrict__ unchanged, int* __restrict__ classes, long cls_ld,
                                              int* __restrict__ n_stopped, double* __restrict__ SHP,
                                              int* __restrict__ colact, double* __restrict__ Hstat, HupdSmem& sm) {
-#ifndef NMFC_HUPD_GSV   // chunk-partial values in flight per thread (32: 128 VGPRs, two workgroups per CU)
-#define NMFC_HUPD_GSV 32
-#endif
-  constexpr int GS = (NMFC_HUPD_GSV / K) < 1 ? 1 : (NMFC_HUPD_GSV / K) > 16 ? 16 : (NMFC_HUPD_GSV / K);
+  // GSV: chunk-partial values in flight per thread (32: 128 VGPRs, two workgroups per CU; 100: every chunk of a
+  // C3-sized restart (10 chunks, k <= 10) in one group of loads, one workgroup per CU -- the latency form)
+  constexpr int GS = (GSV / K) < 1 ? 1 : (GSV / K) > 16 ? 16 : (GSV / K);
   double* sw = sm.sw;
   double* Hn = sm.Hn;
   double* win = sm.win;
@@ -849,10 +848,12 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
   }
 }
 
-#ifndef NMFC_HUPD_MINW   // 4 waves per SIMD: two 512-thread workgroups per CU (full-load launch 150 -> 118 us)
-#define NMFC_HUPD_MINW 4
-#endif
-static __global__ __launch_bounds__(NTH, NMFC_HUPD_MINW) void k_hupdate(int iter, int maxiter, int stop_rule,
+// Two forms (the same arithmetic in the same order, so the same bits): <32, 4> at full load (4 waves per SIMD: two
+// 512-thread workgroups per CU; full-load launch 150 -> 118 us), and <100, 2> when every live restart has a CU of
+// its own (the launch is one chain of dependent loads per restart: all of a restart's chunk partials in flight at
+// once, one workgroup per CU).
+template <int GSV = 32, int MINW = 4>
+static __global__ __launch_bounds__(NTH, MINW) void k_hupdate(int iter, int maxiter, int stop_rule,
                                                         const RestartInfo* __restrict__ ri, int n, long n_pad,
                                                         const double* __restrict__ Gpart, long g_ld, long g_split,
                                                         int nsplit, const double* __restrict__ SWpart, long sw_total,
@@ -867,7 +868,7 @@ static __global__ __launch_bounds__(NTH, NMFC_HUPD_MINW) void k_hupdate(int iter
   if (stop_iter[me.rid] != 0) return;
 #define NMFC_HUPD_CASE(KK)                                                                                      \
   case KK:                                                                                                     \
-    hupdate_body<KK>(me, iter, maxiter, stop_rule, n, n_pad, Gpart, g_ld, g_split, nsplit, SWpart, sw_total, H, SH, \
+    hupdate_body<KK, GSV>(me, iter, maxiter, stop_rule, n, n_pad, Gpart, g_ld, g_split, nsplit, SWpart, sw_total, H, SH, \
                      stop_iter, stop_reason, unchanged, classes, cls_ld, n_stopped, SHP, colact, Hstat, sm);   \
     break;
   switch (me.k) {
