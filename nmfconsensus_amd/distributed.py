@@ -124,11 +124,20 @@ class RestartGroups:
     Engine-like: .m, .n, .device, .run(ks, R, job_begin=, job_end=, counts_tensor=, ...), .close()."""
 
     def __init__(self, A=None, device: int = -1, groups: int = 2, *, a_device_ptr: int | None = None, shape=None,
-                 engine_cls=None):
+                 engine_cls=None, weights=None):
+        """weights: the groups' shares of a job range (default equal; env NMFC_GROUP_WEIGHTS="w0,w1,..." when not
+        given).  Placement never changes a bit, so the split is a speed choice only."""
+        import os
+
         from .nmf import Engine
 
         if not 1 <= groups <= 8:
             raise ValueError("groups must be in 1..8")
+        if weights is None and os.environ.get("NMFC_GROUP_WEIGHTS"):
+            weights = [float(x) for x in os.environ["NMFC_GROUP_WEIGHTS"].split(",")]
+        if weights is not None and (len(weights) != groups or min(weights) <= 0):
+            raise ValueError(f"weights must be {groups} positive numbers")
+        self.weights = None if weights is None else [w / sum(weights) for w in weights]
         cls = engine_cls or Engine
         self.engines = [cls(A, device, a_device_ptr=a_device_ptr, shape=shape) for _ in range(groups)]
         e0 = self.engines[0]
@@ -191,7 +200,15 @@ class RestartGroups:
         if G == 1:
             return self.engines[0].run(ks, R, job_begin=jb, job_end=je, counts_device_ptr=None if counts_tensor is None
                                        else counts_tensor.data_ptr(), **kw)
-        sub = [(jb + (je - jb) * g // G, jb + (je - jb) * (g + 1) // G) for g in range(G)]
+        if self.weights is None or G != self.G:
+            cuts = [jb + (je - jb) * g // G for g in range(G + 1)]
+        else:
+            acc = np.cumsum([0.0] + self.weights)
+            cuts = [jb + int(round((je - jb) * a)) for a in acc]
+            cuts[-1] = je
+        sub = [(cuts[g], cuts[g + 1]) for g in range(G)]
+        if any(b >= e for b, e in sub):   # a group too small for its share: equal split
+            sub = [(jb + (je - jb) * g // G, jb + (je - jb) * (g + 1) // G) for g in range(G)]
         ptrs = [None] * G
         scratch = []
         if counts_tensor is not None:

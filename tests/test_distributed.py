@@ -238,3 +238,17 @@ def test_init_distributed_timeout_default(monkeypatch):
     monkeypatch.setenv("NMFC_DIST_TIMEOUT_S", "42")
     distributed.init_distributed("nccl", device="cuda:0")
     assert seen["timeout"] == datetime.timedelta(seconds=42) and seen["device_id"] == "cuda:0"
+
+
+def test_restart_groups_weights():
+    """Uneven group shares (a speed knob): contiguous sub-ranges in proportion, covering the shard exactly."""
+    from nmfconsensus_amd.distributed import RestartGroups
+    ks, R = [2, 3, 4], 75
+    grp = RestartGroups(np.zeros((10, 5)), device=0, groups=2, engine_cls=_FakeEngine, weights=[8, 1])
+    res = grp.run(ks, R, job_begin=0, job_end=225)
+    calls = sorted(c for e in grp.engines for c in e.calls)
+    assert calls == [(0, 200), (200, 225)]
+    assert np.array_equal(res.iters, np.arange(225))
+    grp.close()
+    with pytest.raises(ValueError):
+        RestartGroups(np.zeros((10, 5)), groups=2, engine_cls=_FakeEngine, weights=[1])
