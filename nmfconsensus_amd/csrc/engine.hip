@@ -309,6 +309,7 @@ struct nmfc_engine {
   DevBuf teamG, teamSW, teamFlag;   // k_team_mu: partial buffers, per-workgroup flags (+ the error word)
   DevBuf solojobs;                  // batched k_solo_mu jobs (small shapes, rank <= 4)
   bool hupd_latency = true;         // env NMFC_HUPD_LATENCY=0: always the full-load k_hupdate form
+  bool narrow_lc = true;            // env NMFC_NARROW_LC=0: the one-wave narrow W^T A kernel
   bool solo_ok = true;              // env NMFC_SOLO=0: no solo kernel (every small-shape restart in k_small_mu blocks)
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // the solo launches (one per kernel rank) beside k_small_mu
   hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
@@ -596,6 +597,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_SMALL")) e->small_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SOLO")) e->solo_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_HUPD_LATENCY")) e->hupd_latency = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_NARROW_LC")) e->narrow_lc = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SMALL_KERNEL"))
     e->small_kernel = std::string(s) == "team" ? 1 : std::string(s) == "single" ? 2 : 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
@@ -1018,10 +1020,16 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           TimedLaunch tl(e, KID_WTA, iter % e->timing_stride == 0);
           if (narrow) {
             const int ntq = (int)(e->n_cols_pad / 16);
-            hipLaunchKernelGGL((k_wta_narrow<16, NARROW_NBUF, true>), dim3(e->nsplit * nblk * (ntq + 1)), dim3(64), 0, st,
-                               e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
-                               e->colinfo.as<ColInfo>(),
-                               e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
+            if (e->narrow_lc)   // loader / consumer waves (bit-identical to the one-wave form)
+              hipLaunchKernelGGL((k_wta_narrow_lc<16, NARROW_NBUF, true>), dim3(e->nsplit * nblk * (ntq + 1)), dim3(128), 0,
+                                 st, e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk,
+                                 nblk, e->colinfo.as<ColInfo>(), e->Gpart.as<double>(), g_ld, g_split,
+                                 e->SWpart.as<double>(), sw_total);
+            else
+              hipLaunchKernelGGL((k_wta_narrow<16, NARROW_NBUF, true>), dim3(e->nsplit * nblk * (ntq + 1)), dim3(64), 0, st,
+                                 e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
+                                 e->colinfo.as<ColInfo>(),
+                                 e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
             auto kw = (ntj >= 4)   ? k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true>

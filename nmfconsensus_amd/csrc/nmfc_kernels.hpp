@@ -620,6 +620,111 @@ static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restri
     for (int reg = 0; reg < 4; ++reg) out[(long)T::row_of(0, reg) * g_ld + T::col_of(nb)] = tl.acc[0][nb][reg];
 }
 
+// Loader / consumer form of k_wta_narrow (round 4): the same items and the same canonical K order (GTile's
+// load_frag / mfma_frag on the same stages), but two waves per item: wave 1 only issues the LDS-DMA stages and waits
+// for them to land, wave 0 only reads fragments and issues the MFMA chain; they meet at one barrier per stage.  In the
+// one-wave form the wave's in-order issue serialises each stage's four 1-KiB DMA pieces (~60 cycles of issue each)
+// with its four dependent MFMAs (~64 cycles each): here the two run on two SIMDs at once.  Bit-identical results.
+template <int RQ, int NBUF, bool ABLK = false>
+static __global__ __launch_bounds__(128) void k_wta_narrow_lc(const double* __restrict__ W, const double* __restrict__ Acm,
+                                                             long m_pad, int ntq, int nsplit, int kchunk, int nblk,
+                                                             const ColInfo* __restrict__ ci, double* __restrict__ Gpart,
+                                                             long g_ld, long g_split, double* __restrict__ SWpart,
+                                                             long sw_total) {
+  static_assert(RQ == 16, "the Gram item shares the tile type: RQ = 16");
+  using T = GTile<16, RQ, 1, 1, NBUF, ABLK>;
+  __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES];
+  const int nt = ntq + 1;   // ntq W^T A tiles + the Gram item
+  const int item = xcd_item(blockIdx.x, nsplit * nblk * nt);
+  const int t = item % nt, bk = (item / nt) % nblk, s = item / (nt * nblk);
+  const int kbeg = s * kchunk;
+  const int kend = (int)min((long)kbeg + kchunk, m_pad);
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
+  const bool gram = t == ntq;
+  const double* Wb = W + (long)bk * 16 * m_pad + kbeg;
+  const long ldq = gram ? m_pad : (ABLK ? (long)ntq * RQ : m_pad);   // operands rebased to the chunk start
+  const double* Q = gram ? Wb : (ABLK ? Acm + (long)kbeg * ldq + (long)t * RQ * 16 : Acm + (long)t * RQ * m_pad + kbeg);
+  const int nst = (kend - kbeg) / BK2;
+  constexpr int D = NBUF - 1;
+  const uint32_t base = (uint32_t)(uintptr_t)smem;
+  T tl;
+  tl.wo = wave;   // each wave is wave 0 of its own 1-wave tile view
+  if (wave == 1) {
+    // loader: the K-blocked A operand only for the W^T A items (the Gram item stages W rows on both sides)
+    if (gram) {
+      GTile<16, RQ, 1, 1, NBUF, false> tg;
+      tg.wo = 1;
+      tg.bind(Wb, m_pad, Q, ldq, kend - kbeg);
+      const int npro = nst < D ? nst : D;
+      for (int q = 0; q < npro; ++q) tg.issue(base + q * T::STAGE_BYTES, q * BK2);
+      T::template wait_stages<D - 1, 0>(npro - 1, false);
+      step_barrier();
+      for (int st = 0; st + 1 < nst; ++st) {
+        if (st + D < nst) tg.issue(base + ((st + D) % NBUF) * T::STAGE_BYTES, (st + D) * BK2);
+        const int left = nst - st - 2;
+        T::template wait_stages<D - 1, 0>(left < D - 1 ? left : D - 1, false);
+        step_barrier();
+      }
+    } else {
+      tl.bind(Wb, m_pad, Q, ldq, kend - kbeg);
+      const int npro = nst < D ? nst : D;
+      for (int q = 0; q < npro; ++q) tl.issue(base + q * T::STAGE_BYTES, q * BK2);
+      T::template wait_stages<D - 1, 0>(npro - 1, false);
+      step_barrier();
+      for (int st = 0; st + 1 < nst; ++st) {
+        if (st + D < nst) tl.issue(base + ((st + D) % NBUF) * T::STAGE_BYTES, (st + D) * BK2);
+        const int left = nst - st - 2;
+        T::template wait_stages<D - 1, 0>(left < D - 1 ? left : D - 1, false);
+        step_barrier();
+      }
+    }
+    return;
+  }
+  // consumer: GTile::run's split steps (kk = 1 MFMAs of stage st behind the barrier publishing stage st + 1)
+  tl.zero();
+  step_barrier();
+  typename T::Frag f0, f1;
+  int b = 0;
+  tl.load_frag(smem, 0, f0);
+  for (int st = 0; st + 1 < nst; ++st) {
+    const char* cur = smem + b * T::STAGE_BYTES;
+    tl.load_frag(cur, 1, f1);
+    tl.mfma_frag(f0);
+    const int bn = (b + 1 == NBUF) ? 0 : b + 1;
+    __builtin_amdgcn_sched_barrier(0);
+    step_barrier();
+    tl.load_frag(smem + bn * T::STAGE_BYTES, 0, f0);
+    __builtin_amdgcn_sched_barrier(0);
+    tl.mfma_frag(f1);
+    b = bn;
+  }
+  {
+    const char* cur = smem + b * T::STAGE_BYTES;
+    tl.load_frag(cur, 1, f1);
+    tl.mfma_frag(f0);
+    tl.mfma_frag(f1);
+  }
+  if (gram) {
+    double* so = SWpart + (long)s * sw_total;
+    const ColInfo* cb = ci + (long)bk * 16;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int lr = g + 4 * reg, lcn = fr;
+      const ColInfo cr = cb[lr];
+      if (cr.k == 0 || cr.lc0 != cb[lcn].lc0 || cb[lcn].k == 0) continue;   // not the same restart
+      const int a = lr - (cr.lc0 & 15), bb = lcn - (cr.lc0 & 15);
+      so[cr.sq_off + a * cr.k + bb] = tl.acc[0][0][reg];
+      so[cr.sq_off + bb * cr.k + a] = tl.acc[0][0][reg];
+    }
+    return;
+  }
+  double* out = Gpart + (long)s * g_split + (long)bk * 16 * g_ld + (long)t * RQ;
+#pragma unroll
+  for (int nb = 0; nb < T::NB; ++nb)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) out[(long)T::row_of(0, reg) * g_ld + T::col_of(nb)] = tl.acc[0][nb][reg];
+}
+
 // ---------------------------------------------------------------------------------------------
 // K2 "hupdate": one workgroup per active restart.
 //   work1 = W0^T W0 = sum of the per-chunk Gram partials (nmf_mu.c:176); work2 = work1 H0 (:178);
