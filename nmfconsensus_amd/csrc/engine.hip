@@ -29,7 +29,7 @@ using namespace nmfc;
 int nmfc_solo_batch_rank(int n, int k);
 int nmfc_solo_batch_launch(const double* Acm, long a_ld, int m, int n, double* W, long w_ld, double* H, long h_ld,
                            const nmfc::SoloJob* djobs, int njobs, int kp, int maxiter, int stop_rule, int* stop_iter,
-                           int* stop_reason, hipStream_t st);
+                           int* stop_reason, int max_wgs, hipStream_t st);
 
 namespace {
 
@@ -956,6 +956,10 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         // beside k_small_mu on streams of their own (one launch per kernel rank), after it when teams run (a team's
         // workgroups must all be resident at once: nothing else may hold CUs then)
         HCHECK(hipEventRecord(e->fork_ev, st));
+        // at most the CUs k_small_mu leaves free (one workgroup of either kernel fills a CU), shared by the solo
+        // launches in proportion to their jobs: the block kernel's workgroups -- the sweep's critical path on C2 --
+        // never wait for a CU behind solo workgroups; a solo workgroup runs its share of jobs one after another
+        const long free_cu = team ? e->ncu : std::max<long>(1, e->ncu - (long)sblocks.size());
         size_t g0 = 0;
         for (int q = 0; g0 < solo.size(); ++q) {
           const int kp = nmfc_solo_batch_rank(n, solo[g0].k);
@@ -965,7 +969,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
           if (!team) HCHECK(hipStreamWaitEvent(sq, e->fork_ev, 0));
           if (nmfc_solo_batch_launch(e->Acm.as<double>(), e->m_pad, m, n, e->W[0].as<double>(), e->m_pad,
                                      e->H[0].as<double>(), e->n_pad, e->solojobs.as<SoloJob>() + g0, (int)(g1 - g0), kp,
-                                     opts.maxiter, opts.stop_rule, e->stop_iter.as<int>(), e->stop_reason.as<int>(), sq))
+                                     opts.maxiter, opts.stop_rule, e->stop_iter.as<int>(), e->stop_reason.as<int>(),
+                                     (int)std::max<long>(1, free_cu * (long)(g1 - g0) / (long)solo.size()), sq))
             return -1;
           if (!team) {
             HCHECK(hipEventRecord(e->join_ev[q], sq));

@@ -90,30 +90,26 @@ struct SoloLayout {
   const nmfc::SoloJob* jobs;   // nullptr: one restart
   int* stop_iter;
   int* stop_reason;
+  int njobs;                   // batched: jobs in `jobs` (the grid may hold fewer workgroups)
 };
 
-template <int NCG, int KK, int SKIP = 0, int SBO = 0, int SL = 0>
+// JOBS: the batched form's job loop (its registers stay out of the single-restart form, whose gct k = 2 case is at
+// the 256-VGPR edge); both forms run the same arithmetic.
+template <int NCG, int KK, int SKIP = 0, int SBO = 0, int SL = 0, bool JOBS = false>
 __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restrict__ A, int m, int n,
                                                          double* __restrict__ W, double* __restrict__ H, int maxiter,
-                                                         int stop_rule, int* __restrict__ state, int kt,
+                                                         int stop_rule, int* __restrict__ state, int kt_arg,
                                                          long long* __restrict__ prof, SoloLayout lay) {
   // gene steps per F batch: larger means fewer H reads from LDS but more live registers (A holds most of them)
   constexpr int SB = SBO ? SBO : KK == 2 ? 8 : 4;
   __shared__ SoloSmem<NCG> sm;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, K = l >> 4, bq = (l >> 2) & 3, j = l & 3;
-  int rid = -1;
-  if (lay.jobs) {   // batched: this workgroup's restart
-    const nmfc::SoloJob jb = lay.jobs[blockIdx.x];
-    W += (long)jb.col0 * lay.w_ld;
-    H += (long)jb.col0 * lay.h_sa;
-    kt = jb.k;
-    rid = jb.rid;
-  }
   constexpr int SR = SOLO_S - SL;   // gene steps of A in registers
   __shared__ double Al[SL > 0 ? SL : 1][NCG][64 * SOLO_W];   // steps SR.. of A, lane-contiguous
   double a_[SR > 0 ? SR : 1][NCG], w_[SOLO_S];
   // A[gene(s)][4 cg + j] from registers (s < SR) or LDS; s, cg compile-time after unrolling
   auto av = [&](int s, int cg) -> double { return s < SR ? a_[s < SR ? s : 0][cg] : Al[s < SR ? 0 : s - SR][cg][tid]; };
+  // A once per workgroup: a batched workgroup runs its jobs one after another on the same A
 #pragma unroll
   for (int s = 0; s < SOLO_S; ++s) {
     const int g = 128 * w + 16 * s + 4 * bq + K;
@@ -126,8 +122,27 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
       else
         Al[s < SR ? 0 : s - SR][cg][tid] = v;
     }
-    w_[s] = (g < m && j < kt) ? W[(long)j * lay.w_ld + g] : 0.0;   // rows kt .. KK - 1: zero padding
   }
+  // batched: jobs blockIdx.x, blockIdx.x + gridDim.x, ... (the grid may be smaller than the job list, so the solo
+  // launches leave CUs to the kernels beside them); one restart otherwise
+  const int njobs = JOBS ? lay.njobs : 1;
+  for (int jx = JOBS ? (int)blockIdx.x : 0; jx < njobs; jx += JOBS ? (int)gridDim.x : 1) {
+  double* __restrict__ Wj = W;
+  double* __restrict__ Hj = H;
+  int kt = kt_arg, rid = -1;
+  if constexpr (JOBS) {
+    const nmfc::SoloJob jb = lay.jobs[jx];
+    Wj = W + (long)jb.col0 * lay.w_ld;
+    Hj = H + (long)jb.col0 * lay.h_sa;
+    kt = jb.k;
+    rid = jb.rid;
+  }
+#pragma unroll
+  for (int s = 0; s < SOLO_S; ++s) {
+    const int g = 128 * w + 16 * s + 4 * bq + K;
+    w_[s] = (g < m && j < kt) ? Wj[(long)j * lay.w_ld + g] : 0.0;   // rows kt .. KK - 1: zero padding
+  }
+  __syncthreads();   // the previous job's last reads of sm are done
   for (int x = tid; x < 2 * SOLO_NCOLP * 4; x += 64 * SOLO_W) (&sm.Hc[0][0][0])[x] = 0.0;
   if (tid == 0) {
     sm.stop = 0;
@@ -136,7 +151,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
   __syncthreads();
   for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
     const int c = x / kt, a = x - c * kt;
-    sm.Hc[0][c][a] = H[(long)c * lay.h_sc + (long)a * lay.h_sa];
+    sm.Hc[0][c][a] = Hj[(long)c * lay.h_sc + (long)a * lay.h_sa];
   }
   __syncthreads();
   long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = 0;
@@ -362,14 +377,14 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
 #pragma unroll
   for (int s = 0; s < SOLO_S; ++s) {
     const int g = 128 * w + 16 * s + 4 * bq + K;
-    if (g < m && j < kt) W[(long)j * lay.w_ld + g] = w_[s];
+    if (g < m && j < kt) Wj[(long)j * lay.w_ld + g] = w_[s];
   }
   for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
     const int c = x / kt, a = x - c * kt;
-    H[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][a];
+    Hj[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][a];
   }
   if (tid == 0) {
-    if (rid >= 0) {
+    if constexpr (JOBS) {
       lay.stop_iter[rid] = sm.stop;
       lay.stop_reason[rid] = sm.reason;
     } else {
@@ -377,13 +392,18 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
       state[1] = sm.reason;
     }
   }
+  }   // jobs
 }
 
 template <int NCG, int KK, int SL = 0>
 hipError_t launch(int grid, const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule, int* st,
                   int kt, const SoloLayout& lay, hipStream_t s) {
-  hipLaunchKernelGGL((k_solo_mu<NCG, KK, 0, 0, SL>), dim3(grid), dim3(64 * SOLO_W), 0, s, A, m, n, W, H, maxiter,
-                     stop_rule, st, kt, nullptr, lay);
+  if (lay.jobs)
+    hipLaunchKernelGGL((k_solo_mu<NCG, KK, 0, 0, SL, true>), dim3(grid), dim3(64 * SOLO_W), 0, s, A, m, n, W, H, maxiter,
+                       stop_rule, st, kt, nullptr, lay);
+  else
+    hipLaunchKernelGGL((k_solo_mu<NCG, KK, 0, 0, SL, false>), dim3(grid), dim3(64 * SOLO_W), 0, s, A, m, n, W, H,
+                       maxiter, stop_rule, st, kt, nullptr, lay);
   return hipGetLastError();
 }
 
@@ -536,7 +556,7 @@ int mu_solo_call(const double* A, int m, int n, int k, int maxiter, int stop_rul
   int* dstate = reinterpret_cast<int*>(g.dwork);
   double* dW = g.dwork + 2;
   double* dH = dW + lw;
-  const SoloLayout lay{m, m, kp, 1, nullptr, nullptr, nullptr};
+  const SoloLayout lay{m, m, kp, 1, nullptr, nullptr, nullptr, 1};
   SCHECK(dispatch(1, kp, g.dA, m, n, dW, dH, maxiter, stop_rule, dstate, k, lay, g.st));
   SCHECK(hipMemcpyAsync(g.pin, g.dwork, need * sizeof(double), hipMemcpyDeviceToHost, g.st));
   SCHECK(hipStreamSynchronize(g.st));
@@ -555,22 +575,24 @@ int mu_solo_call(const double* A, int m, int n, int k, int maxiter, int stop_rul
 }
 }  // namespace
 
-// Batched form (nmfc_engine_run, small shapes): one workgroup per job of kernel rank kp (solo_rank(n, k) == kp for
-// every job; the engine groups its solo jobs by kp), reading the engine's column-major Acm and the stacked W/H at
-// each job's col0, stop state into stop_iter / stop_reason[rid].  Returns 0 or -1 (nmfc_last_error).
+// Batched form (nmfc_engine_run, small shapes): jobs of kernel rank kp (solo_rank(n, k) == kp for every job; the
+// engine groups its solo jobs by kp) on min(njobs, max_wgs) workgroups, each running its jobs one after another,
+// reading the engine's column-major Acm and the stacked W/H at each job's col0, stop state into stop_iter /
+// stop_reason[rid].  Returns 0 or -1 (nmfc_last_error).
 __attribute__((visibility("hidden"))) int nmfc_solo_batch_rank(int n, int k) { return solo_rank(n, k); }
 
 __attribute__((visibility("hidden"))) int nmfc_solo_batch_launch(const double* Acm, long a_ld, int m, int n, double* W,
                                                                  long w_ld, double* H, long h_ld,
                                                                  const nmfc::SoloJob* djobs, int njobs, int kp,
                                                                  int maxiter, int stop_rule, int* stop_iter,
-                                                                 int* stop_reason, hipStream_t st) {
+                                                                 int* stop_reason, int max_wgs, hipStream_t st) {
   if (njobs <= 0) return 0;
   if (!nmfc_mu_solo_fits(m, n, 2) || kp < 2 || kp > 4) {
     nmfc_set_error("nmfc_solo_batch_launch: shape outside the solo kernel's range");
     return -1;
   }
-  const SoloLayout lay{a_ld, w_ld, 1, h_ld, djobs, stop_iter, stop_reason};
-  SCHECK(dispatch(njobs, kp, Acm, m, n, W, H, maxiter, stop_rule, nullptr, kp, lay, st));
+  const SoloLayout lay{a_ld, w_ld, 1, h_ld, djobs, stop_iter, stop_reason, njobs};
+  const int grid = std::max(1, std::min(njobs, max_wgs > 0 ? max_wgs : njobs));
+  SCHECK(dispatch(grid, kp, Acm, m, n, W, H, maxiter, stop_rule, nullptr, kp, lay, st));
   return 0;
 }
