@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -310,6 +311,7 @@ struct nmfc_engine {
   DevBuf solojobs;                  // batched k_solo_mu jobs (small shapes, rank <= 4)
   bool hupd_latency = true;         // env NMFC_HUPD_LATENCY=0: always the full-load k_hupdate form
   bool narrow_lc = true;            // env NMFC_NARROW_LC=0: the one-wave narrow W^T A kernel
+  bool gram_model = true;           // env NMFC_GRAM_MODEL=0: the tile cost model without the Gram workgroups
   bool solo_ok = true;              // env NMFC_SOLO=0: no solo kernel (every small-shape restart in k_small_mu blocks)
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // the solo launches (one per kernel rank) beside k_small_mu
   hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
@@ -361,18 +363,23 @@ struct TileChoice {
 TileChoice choose_tiles(const nmfc_engine* e, int np_live, int ntj) {
   const long ns = e->nsplit, cu = e->ncu;
   const long np = std::max(np_live, 1);
+  // The 1-panel shapes launch 3 Gram workgroups per (chunk, panel) beside their tiles (GITEM): one 512-MFMA chain
+  // per wave, about a quarter of a 1 x 64 tile's work and half of a 1 x 32 tile's, counted as such (round 4: without
+  // them the model chose 1 x 64 tiles at 9..12 live panels, 295 us per launch on the R = 25 shard against 275 for
+  // 2-panel tiles, and 1 x 32 tiles at 6, 191 us against ~165; profiles/r04/shard2_wta_shapes.txt).
   struct Cand {
     int id;
-    long wgs, slots;
+    double wgs;
+    long slots;
     double t;
-  } cands[4] = {{0, ns * ((np + 3) / 4) * ntj, cu, 2.0},
-                {3, ns * ((np + 1) / 2) * ntj, cu, 1.0},
-                {1, ns * np * 2 * ntj, 3 * cu, 0.8},
-                {2, ns * np * 4 * ntj, 4 * cu, 0.6}};
+  } cands[4] = {{0, (double)(ns * ((np + 3) / 4) * ntj), cu, 2.0},
+                {3, (double)(ns * ((np + 1) / 2) * ntj), cu, 1.0},
+                {1, (double)(ns * np) * (2 * ntj + (e->gram_model ? 0.75 : 0.0)), 3 * cu, 0.8},
+                {2, (double)(ns * np) * (4 * ntj + (e->gram_model ? 1.5 : 0.0)), 4 * cu, 0.6}};
   TileChoice tc{0, false};
   double best = 1e300;
   for (const Cand& c : cands) {
-    const double est = (double)((c.wgs + c.slots - 1) / c.slots) * c.t;
+    const double est = std::ceil(c.wgs / (double)c.slots) * c.t;
     if (est < best - 1e-9) {
       best = est;
       tc.wta = c.id;
@@ -598,6 +605,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_SOLO")) e->solo_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_HUPD_LATENCY")) e->hupd_latency = atoi(s) != 0;
   if (const char* s = getenv("NMFC_NARROW_LC")) e->narrow_lc = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_GRAM_MODEL")) e->gram_model = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SMALL_KERNEL"))
     e->small_kernel = std::string(s) == "team" ? 1 : std::string(s) == "single" ? 2 : 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
