@@ -309,7 +309,6 @@ struct nmfc_engine {
   DevBuf initjobs, chunk_job, chunk_idx, jump, labels, slot, grp_begin, grp_list, counts_tmp, cons_tmp, smallblk;
   DevBuf teamG, teamSW, teamFlag;   // k_team_mu: partial buffers, per-workgroup flags (+ the error word)
   DevBuf solojobs;                  // batched k_solo_mu jobs (small shapes, rank <= 4)
-  bool hupd_latency = true;         // env NMFC_HUPD_LATENCY=0: always the full-load k_hupdate form
   bool narrow_lc = true;            // env NMFC_NARROW_LC=0: the one-wave narrow W^T A kernel
   bool gram_model = true;           // env NMFC_GRAM_MODEL=0: the tile cost model without the Gram workgroups
   bool solo_ok = true;              // env NMFC_SOLO=0: no solo kernel (every small-shape restart in k_small_mu blocks)
@@ -603,7 +602,6 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_NARROW_MAXB")) e->narrow_maxb = std::min(8, std::max(1, atoi(s)));
   if (const char* s = getenv("NMFC_SMALL")) e->small_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SOLO")) e->solo_ok = atoi(s) != 0;
-  if (const char* s = getenv("NMFC_HUPD_LATENCY")) e->hupd_latency = atoi(s) != 0;
   if (const char* s = getenv("NMFC_NARROW_LC")) e->narrow_lc = atoi(s) != 0;
   if (const char* s = getenv("NMFC_GRAM_MODEL")) e->gram_model = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SMALL_KERNEL"))
@@ -959,11 +957,13 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     {
       TimedLaunch tl(e, KID_SMALL);   // the whole small-shape phase: k_small_mu blocks and the solo launches
       const bool team = use_team(e, (int)sblocks.size());
+      // the fork point is recorded BEFORE the block kernel: an event recorded after it would hold the solo launches
+      // until the block kernel had finished (round 4: C1 24.7 ms = 9.9 + 14.8 ms serialised)
+      if (!solo.empty() && !team) HCHECK(hipEventRecord(e->fork_ev, st));
       if (!sblocks.empty() && launch_small(e, (int)sblocks.size(), opts.maxiter, opts.stop_rule)) return -1;
       if (!solo.empty()) {
         // beside k_small_mu on streams of their own (one launch per kernel rank), after it when teams run (a team's
         // workgroups must all be resident at once: nothing else may hold CUs then)
-        HCHECK(hipEventRecord(e->fork_ev, st));
         // at most the CUs k_small_mu leaves free (one workgroup of either kernel fills a CU), shared by the solo
         // launches in proportion to their jobs: the block kernel's workgroups -- the sweep's critical path on C2 --
         // never wait for a CU behind solo workgroups; a solo workgroup runs its share of jobs one after another
@@ -1081,9 +1081,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         }
         {
           TimedLaunch tl(e, KID_HUPD, iter % e->timing_stride == 0);
-          // one workgroup per live restart: the latency form when each has a CU of its own (same bits)
-          auto kh = (nact <= e->ncu && e->hupd_latency) ? k_hupdate<100, 2> : k_hupdate<32, 4>;
-          hipLaunchKernelGGL(kh, dim3(nact), dim3(NTH), 0, st, iter, opts.maxiter, opts.stop_rule,
+          hipLaunchKernelGGL(k_hupdate<>, dim3(nact), dim3(NTH), 0, st, iter, opts.maxiter, opts.stop_rule,
                              e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, e->nsplit,
                              e->SWpart.as<double>(), sw_total, e->H[cur].as<double>(), e->SH.as<double>(),
                              e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->unchanged.as<int>(),

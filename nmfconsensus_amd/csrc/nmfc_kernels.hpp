@@ -757,8 +757,9 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
                                              int* __restrict__ unchanged, int* __restrict__ classes, long cls_ld,
                                              int* __restrict__ n_stopped, double* __restrict__ SHP,
                                              int* __restrict__ colact, double* __restrict__ Hstat, HupdSmem& sm) {
-  // GSV: chunk-partial values in flight per thread (32: 128 VGPRs, two workgroups per CU; 100: every chunk of a
-  // C3-sized restart (10 chunks, k <= 10) in one group of loads, one workgroup per CU -- the latency form)
+  // GSV: chunk-partial values in flight per thread (32: 128 VGPRs, two workgroups per CU).  Round 4 measured a
+  // "latency form" <100, 2> (every chunk of a C3 restart in one group of loads, one workgroup per CU) for launches
+  // of at most one restart per CU: the 8-GPU replay went 380.8 -> 373.3 per GPU, so it is not used.
   constexpr int GS = (GSV / K) < 1 ? 1 : (GSV / K) > 16 ? 16 : (GSV / K);
   double* sw = sm.sw;
   double* Hn = sm.Hn;
@@ -953,10 +954,7 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
   }
 }
 
-// Two forms (the same arithmetic in the same order, so the same bits): <32, 4> at full load (4 waves per SIMD: two
-// 512-thread workgroups per CU; full-load launch 150 -> 118 us), and <100, 2> when every live restart has a CU of
-// its own (the launch is one chain of dependent loads per restart: all of a restart's chunk partials in flight at
-// once, one workgroup per CU).
+// <32, 4>: 4 waves per SIMD, two 512-thread workgroups per CU (full-load launch 150 -> 118 us).
 template <int GSV = 32, int MINW = 4>
 static __global__ __launch_bounds__(NTH, MINW) void k_hupdate(int iter, int maxiter, int stop_rule,
                                                         const RestartInfo* __restrict__ ri, int n, long n_pad,

@@ -134,7 +134,8 @@ class RestartGroups:
         if not 1 <= groups <= 8:
             raise ValueError("groups must be in 1..8")
         if weights is None and os.environ.get("NMFC_GROUP_WEIGHTS"):
-            weights = [float(x) for x in os.environ["NMFC_GROUP_WEIGHTS"].split(",")]
+            env = [float(x) for x in os.environ["NMFC_GROUP_WEIGHTS"].split(",")]
+            weights = env if len(env) == groups else None   # the knob names a split for one group count
         if weights is not None and (len(weights) != groups or min(weights) <= 0):
             raise ValueError(f"weights must be {groups} positive numbers")
         self.weights = None if weights is None else [w / sum(weights) for w in weights]
