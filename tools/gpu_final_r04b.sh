@@ -9,7 +9,7 @@ for C in C1 C2; do
   timeout -k 10 300 python -u bench.py --config $C --steps 10 --warmup 2 > "$OUT/${C,,}_bench.json" 2> "$OUT/${C,,}_bench.err" \
     && echo "$C ok" || { tail -5 "$OUT/${C,,}_bench.err"; exit 1; }
 done
-timeout -k 10 600 python -u bench.py --config C4 --steps 1 --warmup 1 > "$OUT/c4_bench.json" 2> "$OUT/c4_bench.err" \
+timeout -k 10 600 python -u bench.py --config C4 --steps 1 --warmup 1 --cpu-iters 4 > "$OUT/c4_bench.json" 2> "$OUT/c4_bench.err" \
   && echo "C4 ok" || { tail -5 "$OUT/c4_bench.err"; exit 1; }
 timeout -k 10 600 python -u bench.py --config C5 --steps 1 --warmup 1 > "$OUT/c5_bench.json" 2> "$OUT/c5_bench.err" \
   && echo "C5 ok" || { tail -5 "$OUT/c5_bench.err"; exit 1; }
