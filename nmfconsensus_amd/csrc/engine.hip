@@ -311,7 +311,6 @@ struct nmfc_engine {
   DevBuf solojobs;                  // batched k_solo_mu jobs (small shapes, rank <= 4)
   bool narrow_lc = true;            // env NMFC_NARROW_LC=0: the one-wave narrow W^T A kernel
   bool gram_model = true;           // env NMFC_GRAM_MODEL=0: the tile cost model without the Gram workgroups
-  bool gram_il = true;              // env NMFC_GRAM_IL=0: Gram chains as a block after each stage's kk = 0 MFMAs
   bool solo_ok = true;              // env NMFC_SOLO=0: no solo kernel (every small-shape restart in k_small_mu blocks)
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // the solo launches (one per kernel rank) beside k_small_mu
   hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
@@ -605,7 +604,6 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_SOLO")) e->solo_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_NARROW_LC")) e->narrow_lc = atoi(s) != 0;
   if (const char* s = getenv("NMFC_GRAM_MODEL")) e->gram_model = atoi(s) != 0;
-  if (const char* s = getenv("NMFC_GRAM_IL")) e->gram_il = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SMALL_KERNEL"))
     e->small_kernel = std::string(s) == "team" ? 1 : std::string(s) == "single" ? 2 : 0;
   if (const char* s = getenv("NMFC_AHTW_TILE")) {
@@ -1047,12 +1045,9 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                  e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
-            auto kw = e->gram_il ? ((ntj >= 4)   ? k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true, true, false, true>
-                                    : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2, GT_NBUF, 1, true, true, false, true>
-                                                 : k_wta2<WTA_NPT, 128, 4, 2, 4, GT_NBUF, 1, true, true, false, true>)
-                                 : ((ntj >= 4)   ? k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true>
-                                    : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2, GT_NBUF, 1, true>
-                                                 : k_wta2<WTA_NPT, 128, 4, 2, 4, GT_NBUF, 1, true>);
+            auto kw = (ntj >= 4)   ? k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true>
+                      : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2, GT_NBUF, 1, true>
+                                   : k_wta2<WTA_NPT, 128, 4, 2, 4, GT_NBUF, 1, true>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
                                e->Ablk.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
@@ -1060,10 +1055,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                sw_total);
           } else if (wta_mid) {   // npanels is a multiple of WTA_NPT, so of 2
             const int ng = (lp + 1) / 2;
-            auto kw = e->gram_il ? ((ntj >= 2) ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW, true, true, false, true>
-                                               : k_wta2<2, 128, 4, 2, 2, WTA_MID_NBUF, WTA_MID_MINW, true, true, false, true>)
-                                 : ((ntj >= 2) ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW, true>
-                                               : k_wta2<2, 128, 4, 2, 2, WTA_MID_NBUF, WTA_MID_MINW, true>);
+            auto kw = (ntj >= 2) ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW, true>
+                                 : k_wta2<2, 128, 4, 2, 2, WTA_MID_NBUF, WTA_MID_MINW, true>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
                                e->Ablk.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),

@@ -182,69 +182,6 @@ struct GTile {
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].y, f.b[j].y, acc[i][j], 0, 0, 0);
   }
-  // mfma_frag with a hook after the x half and after the y half (hook(0), hook(1)): another accumulator's MFMAs
-  // issued between independent tile MFMAs, so their dependent chain never stalls the wave at the barrier
-  template <class Hook>
-  __device__ __forceinline__ void mfma_frag_hooked(const Frag& f, Hook hook, int phase0) {
-#pragma unroll
-    for (int i = 0; i < MB; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].x, f.b[j].x, acc[i][j], 0, 0, 0);
-    hook(phase0);
-#pragma unroll
-    for (int i = 0; i < MB; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].y, f.b[j].y, acc[i][j], 0, 0, 0);
-    hook(phase0 + 1);
-  }
-
-  // The NBUF >= 3 K loop of run() with a side chain interleaved: `load(stage)` reads the side chain's operands of
-  // a stage (before the barrier after which the stage may be overwritten), `step(q)` issues its MFMA q of the stage
-  // (q = 0, 1: the kk = 0 x / y halves, right behind the tile's kk = 0 x / y MFMAs; q = 2, 3: kk = 1, behind the
-  // tile's kk = 1 halves).  The tile's and the side chain's accumulators each see exactly run()'s order.
-  template <class Load, class Step>
-  __device__ __forceinline__ void run_side(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
-                                           int kbeg, int kend, char* __restrict__ smem, Load load, Step step) {
-    static_assert(NBUF >= 3, "the side-chain loop is the ring form");
-    const int nst = (kend - kbeg) / BK2;
-    bind(P, ldp, Q, ldq, kend);
-    const uint32_t base = (uint32_t)(uintptr_t)smem;
-    constexpr int D = NBUF - 1;
-    const int npro = nst < D ? nst : D;
-    for (int q = 0; q < npro; ++q) issue(base + q * STAGE_BYTES, kbeg + q * BK2);
-    wait_stages<D - 1, 0>(npro - 1, false);
-    step_barrier();
-    int b = 0;
-    Frag f0, f1;
-    load_frag(smem, 0, f0);
-    for (int s = 0; s + 1 < nst; ++s) {
-      const char* cur = smem + b * STAGE_BYTES;
-      if (s + D < nst) {
-        const int bd = (b + D >= NBUF) ? b + D - NBUF : b + D;
-        issue(base + bd * STAGE_BYTES, kbeg + (s + D) * BK2);
-      }
-      load_frag(cur, 1, f1);
-      load(cur);
-      mfma_frag_hooked(f0, step, 0);
-      const int bn = (b + 1 == NBUF) ? 0 : b + 1;
-      const int left = nst - s - 2;
-      __builtin_amdgcn_sched_barrier(0);
-      wait_stages<D - 1, 0>(left < D - 1 ? left : D - 1, false);
-      step_barrier();
-      load_frag(smem + bn * STAGE_BYTES, 0, f0);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_frag_hooked(f1, step, 2);
-      b = bn;
-    }
-    {
-      const char* cur = smem + b * STAGE_BYTES;
-      load_frag(cur, 1, f1);
-      load(cur);
-      mfma_frag_hooked(f0, step, 0);
-      mfma_frag_hooked(f1, step, 2);
-    }
-  }
-
   __device__ __forceinline__ void compute(const char* __restrict__ st) {
     const int w = (threadIdx.x >> 6) - wo, l = threadIdx.x & 63;
     const int wr = w / WC, wc = w % WC;
@@ -473,10 +410,8 @@ __device__ __forceinline__ void gram_cand(int cand, int& q, int& br, int& bc) {
   }
 }
 
-// GIL (round 4): the Gram chains interleaved with the tile's MFMAs (GTile::run_side) instead of run as a block after
-// each stage's kk = 0 MFMAs, where their dependent chain held the carrying waves -- and the barrier -- behind.
 template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1, bool ABLK = false, bool GRAM = true,
-          bool GITEM = false, bool GIL = false>
+          bool GITEM = false>
 static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
                                                               long m_pad, int ngroups, int ntj, int nsplit, int kchunk,
                                                               const int* __restrict__ prb, const int* __restrict__ pre,
@@ -582,35 +517,6 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
     }
   }
   const double* P = W + (long)pg * 64 * NPT * m_pad + kbeg;
-  if constexpr (GIL && GRAM && !GITEM) {
-    // the stage's Gram operands, both kk halves, read before the barrier that frees the stage
-    d2 ga[GPW][2], gb[GPW][2];
-    tl.run_side(P, m_pad, Q, ldq, 0, kend - kbeg, smem,
-                [&](const char* stg) {
-                  if (!gram) return;
-#pragma unroll
-                  for (int x = 0; x < GPW; ++x) {
-                    if (!my_need[x]) continue;
-                    const char* pa = stg + (my_ra[x] + fr) * 128;
-                    const char* pb = stg + (my_rb[x] + fr) * 128;
-#pragma unroll
-                    for (int kk = 0; kk < 2; ++kk) {
-                      const int so = ((4 * kk + g) ^ (fr >> 1)) << 4;
-                      ga[x][kk] = *reinterpret_cast<const d2*>(pa + so);
-                      gb[x][kk] = *reinterpret_cast<const d2*>(pb + so);
-                    }
-                  }
-                },
-                [&](int q) {   // q: kk = q >> 1, x / y half = q & 1 -- per stage kk0.x, kk0.y, kk1.x, kk1.y as run()
-                  if (!gram) return;
-#pragma unroll
-                  for (int x = 0; x < GPW; ++x) {
-                    if (!my_need[x]) continue;
-                    const d2 a = ga[x][q >> 1], b = gb[x][q >> 1];
-                    gacc[x] = __builtin_amdgcn_mfma_f64_16x16x4f64((q & 1) ? a.y : a.x, (q & 1) ? b.y : b.x, gacc[x], 0, 0, 0);
-                  }
-                });
-  } else {
   tl.run(P, m_pad, Q, ldq, 0, kend - kbeg, smem, [&](const char* stg) {
     if (!gram) return;
 #pragma unroll
@@ -628,7 +534,6 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
       }
     }
   });
-  }
   double* out = Gpart + (long)s * g_split + (long)pg * 64 * NPT * g_ld + (long)t * RQ;
 #pragma unroll
   for (int mb = 0; mb < T::MB; ++mb)
