@@ -3,7 +3,7 @@
 The product is nmfconsensus_amd/libnmf.so (HIP/gfx950, C ABI in include/).  This package holds its
 Python bindings and the host-side mirror of the reference's R driver (nmf.r).
 """
-from .gct import GCT, read_dataset, read_gct, write_gct  # noqa: F401
+from .gct import GCT, read_dataset, read_gct, read_res, write_gct  # noqa: F401
 
 __version__ = "0.1.0"
 

@@ -1,6 +1,9 @@
-"""GCT 1.2 dataset I/O -- mirror of nmf.r's read.gct / write.gct / read.dataset.
+"""GCT 1.2 / RES dataset I/O -- mirror of nmf.r's read.gct / read.res / write.gct / read.dataset.
 
 read.gct  (nmf.r:371-377): read.delim(skip=2, header=T, row.names=1) then drop the Description column.
+read.res  (nmf.r:351-369): sample labels = header fields 3, 5, 7, ... (1-based; R's strsplit drops a trailing
+                           empty field); body after 3 skipped lines, row names from column 2 (Accession), values
+                           from the even columns after it (the odd ones are the A/P/M calls, dropped).
 write.gct (nmf.r:379-408): "#1.2", dims, a header "Name\tDescription\t1..ncol" + column names, then rows
                            with the row name repeated as Name and Description.
 Values are parsed with Python's correctly rounded float(); R's own R_strtod is not pinned here
@@ -46,10 +49,44 @@ def read_gct(path: str) -> GCT:
     return GCT(data, names, col_names)
 
 
+def read_res(path: str) -> GCT:
+    with open(path, "r") as f:
+        lines = f.read().splitlines()
+    if len(lines) < 3:
+        raise ValueError(f"{path}: not a RES file (fewer than 3 header lines)")
+    head = lines[0].split("\t")
+    while head and head[-1] == "":
+        head.pop()                      # strsplit("a\tb\t", "\t") is c("a", "b")
+    labels = head[2::2]
+    rows, names = [], []
+    for ln in lines[3:]:
+        if not ln.strip():
+            continue                    # blank.lines.skip=T
+        parts = ln.split("\t")
+        if len(parts) < 3:
+            raise ValueError(f"{path}: data line with {len(parts)} fields")
+        names.append(parts[1])          # row.names = 2
+        rows.append([float(x) for x in parts[2::2]])
+    if not rows:
+        raise ValueError(f"{path}: no data lines")
+    ncols = {len(r) for r in rows}
+    if len(ncols) != 1:
+        raise ValueError(f"{path}: ragged data lines ({sorted(ncols)} value columns)")
+    if len(set(names)) != len(names):
+        raise ValueError(f"{path}: duplicate row names (read.delim row.names=2 refuses them)")
+    data = np.array(rows, dtype=np.float64)
+    if data.shape[1] != len(labels):
+        raise ValueError(f"{path}: {len(labels)} sample labels for {data.shape[1]} value columns")
+    return GCT(data, names, labels)
+
+
 def read_dataset(path: str) -> GCT:
-    """nmf.r:261-269: dispatch on the file suffix (.gct only; .res is out of scope)."""
-    if path.lower().endswith(".gct"):
+    """nmf.r:261-269: dispatch on the file suffix, .gct first, then .res (case-insensitive)."""
+    low = path.lower()
+    if low.endswith(".gct"):
         return read_gct(path)
+    if low.endswith(".res"):
+        return read_res(path)
     raise ValueError("Input is not a res or gct file.")
 
 
