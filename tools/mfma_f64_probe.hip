@@ -29,6 +29,33 @@ __global__ void chain_k(const double* A, const double* B, const double* C, doubl
   }
 }
 
+// v_mfma_f64_4x4x4_4b: 4 blocks b of 4 x 4 outputs, K = 4.  Lane 16 K + 4 b + i holds X_b[i][K] and Y_b[K][i]
+// (operand order: D_b = X_b Y_b + C_b); result lane 16 i + 4 b + j holds D_b[i][j].  Is it the k-ordered fma chain?
+__global__ void chain4_k(const double* X, const double* Y, const double* C, double* D, double* Dref) {
+  const int l = threadIdx.x, K = l >> 4, b = (l >> 2) & 3, i = l & 3;
+  const int ri = l >> 4, rj = l & 3;   // result (i, j) of block b for this lane
+  double acc = C[b * 16 + ri * 4 + rj];
+  acc = __builtin_amdgcn_mfma_f64_4x4x4f64(X[b * 16 + i * 4 + K], Y[b * 16 + K * 4 + i], acc, 0, 0, 0);
+  D[b * 16 + ri * 4 + rj] = acc;
+  double s = C[b * 16 + ri * 4 + rj];
+  for (int k = 0; k < 4; ++k) s = fma(X[b * 16 + ri * 4 + k], Y[b * 16 + k * 4 + rj], s);
+  Dref[b * 16 + ri * 4 + rj] = s;
+}
+
+template <int NACC>
+__global__ void rate4_k(double* out, int iters, double seed) {
+  double acc[NACC];
+  for (int i = 0; i < NACC; i++) acc[i] = seed;
+  double a = seed + threadIdx.x * 1e-3, b = seed - threadIdx.x * 1e-3;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int i = 0; i < NACC; i++) acc[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, acc[i], 0, 0, 0);
+  }
+  double s = 0;
+  for (int i = 0; i < NACC; i++) s += acc[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 template <int NACC>
 __global__ void rate_k(double* out, int iters, double seed) {
   d4 acc[NACC];
@@ -96,6 +123,23 @@ int main() {
     }
     printf("f64 MFMA == k-ordered fma chain: %d / %d entries bit-identical\n", same, tot);
   }
+  {
+    double hX[64], hY[64], hC4[64], hD[64], hR[64];
+    unsigned long long x = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return (double)(x >> 11) / 9007199254740992.0 * 2 - 1; };
+    double *dX, *dY, *dC4, *dD4, *dR4;
+    CK(hipMalloc(&dX, 512)); CK(hipMalloc(&dY, 512)); CK(hipMalloc(&dC4, 512)); CK(hipMalloc(&dD4, 512)); CK(hipMalloc(&dR4, 512));
+    int same = 0, tot = 0;
+    for (int trial = 0; trial < 400; ++trial) {
+      for (int i = 0; i < 64; ++i) { hX[i] = rnd() * (1 << (trial % 20)); hY[i] = rnd() / (1 + trial % 7); hC4[i] = rnd() * 1e3; }
+      CK(hipMemcpy(dX, hX, 512, hipMemcpyHostToDevice)); CK(hipMemcpy(dY, hY, 512, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dC4, hC4, 512, hipMemcpyHostToDevice));
+      chain4_k<<<1, 64>>>(dX, dY, dC4, dD4, dR4);
+      CK(hipMemcpy(hD, dD4, 512, hipMemcpyDeviceToHost)); CK(hipMemcpy(hR, dR4, 512, hipMemcpyDeviceToHost));
+      for (int i = 0; i < 64; ++i) { tot++; same += (hD[i] == hR[i]); }
+    }
+    printf("f64 MFMA 4x4x4 == k-ordered fma chain: %d / %d entries bit-identical\n", same, tot);
+  }
   double* dout; CK(hipMalloc(&dout, 1 << 24));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   int iters = 4000; float ms;
@@ -122,6 +166,19 @@ int main() {
       CK(hipEventElapsedTime(&ms, e0, e1));
       printf("mfma f64 one wave/SIMD, %d chain(s): %.1f cycles/mfma @2.4GHz\n", na, ms * 1e-3 * 2.4e9 / (iters * (double)na));
     }
+    for (int na = 1; na <= 4; na *= 2) {   // 4x4x4: one wave per SIMD
+      CK(hipEventRecord(e0));
+      if (na == 1) rate4_k<1><<<256, 256>>>(dout, iters, 1.0);
+      if (na == 2) rate4_k<2><<<256, 256>>>(dout, iters, 1.0);
+      if (na == 4) rate4_k<4><<<256, 256>>>(dout, iters, 1.0);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("mfma f64 4x4x4 one wave/SIMD, %d chain(s): %.1f cycles/mfma @2.4GHz\n", na, ms * 1e-3 * 2.4e9 / (iters * (double)na));
+    }
+    CK(hipEventRecord(e0)); rate4_k<4><<<blocks, threads>>>(dout, iters, 1.0); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    fl = (double)blocks * (threads / 64) * iters * 4 * 512.0;
+    printf("mfma f64 4x4x4, 4 acc, %d WGx%d: %.3f ms  %.2f TFLOP/s\n", blocks, threads, ms, fl / ms / 1e9);
     CK(hipEventRecord(e0)); valu_k<<<blocks, threads>>>(dout, iters, 1.0); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1));
     fl = (double)blocks * threads * iters * 8 * 2.0;
