@@ -149,6 +149,10 @@ constexpr int NARROW_NBUF = NMFC_NARROW_NBUF;      // LDS ring depth of the narr
 #ifndef NMFC_WTA_MID_MINW
 #define NMFC_WTA_MID_MINW 1
 #endif
+#ifndef NMFC_WTA_GREG
+#define NMFC_WTA_GREG 1
+#endif
+constexpr bool WTA_GREG = NMFC_WTA_GREG != 0;      // 4-panel W^T A tiles: diagonal Gram blocks from the tile's W registers
 constexpr int WTA_MID_NBUF = NMFC_WTA_MID_NBUF;    // ring depth of the 2-panel W^T A tile
 constexpr int WTA_MID_MINW = NMFC_WTA_MID_MINW;    // its launch-bounds waves per SIMD (4: two workgroups per CU)
 constexpr int AHTW_NBUF = NMFC_AHTW_NBUF;          // LDS ring depth of the full-width A h^T tiles
@@ -1045,7 +1049,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                  e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
-            auto kw = (ntj >= 4)   ? k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true>
+            auto kw = (ntj >= 4)   ? k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true, true, false, WTA_GREG>
                       : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2, GT_NBUF, 1, true>
                                    : k_wta2<WTA_NPT, 128, 4, 2, 4, GT_NBUF, 1, true>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),

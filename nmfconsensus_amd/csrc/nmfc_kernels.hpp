@@ -87,7 +87,11 @@ __device__ __forceinline__ void step_barrier() {
 // QBLK: the Q operand is K-blocked ([K/16][rows][16] doubles: one 16-gene block of every row
 // contiguous, `ldq` = the total row count), so a stage of a tile is ONE contiguous RQ x 128 B run instead
 // of RQ rows 8 * ldq bytes apart.  The same canonical K order either way.
-template <int RP, int RQ, int WR, int WC, int NBUF = GT_NBUF, bool QBLK = false>
+// GREG: the wave may also accumulate one restart-diagonal 16 x 16 Gram block of its own P rows, block `gsel` of
+// its MB row blocks, into `gacc` -- W^T W from the W fragments already in registers for the tile MFMAs
+// (the A operand lane map (row fr, k g) and the B operand map (k g, col fr) hold the same value for P = Q),
+// in the canonical K order; gsel < 0: none.
+template <int RP, int RQ, int WR, int WC, int NBUF = GT_NBUF, bool QBLK = false, bool GREG = false>
 struct GTile {
   static_assert(NBUF >= 2 && NBUF <= 16, "ring of 2..16 stages");
   static constexpr int NW = WR * WC;
@@ -100,8 +104,11 @@ struct GTile {
   static_assert(PIECES % NW == 0 && (RP / 8) % NW == 0, "pieces must split evenly over waves");
   static constexpr int MB = RP / WR / 16;
   static constexpr int NB = RQ / WC / 16;
+  static_assert(!GREG || NBUF >= 3, "register Gram on the split-step ring only");
 
   d4 acc[MB][NB];
+  d4 gacc;
+  int gsel = -1;   // GREG: wave-uniform
   __amdgpu_buffer_rsrc_t rp, rq;
   int voff[PPW];
   int qkm;
@@ -129,6 +136,7 @@ struct GTile {
     for (int i = 0; i < MB; ++i)
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+    gacc = (d4){0.0, 0.0, 0.0, 0.0};
   }
 
   // DMA of the stage starting at K position k0 into the LDS buffer at byte address `buf`
@@ -181,6 +189,16 @@ struct GTile {
     for (int i = 0; i < MB; ++i)
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].y, f.b[j].y, acc[i][j], 0, 0, 0);
+    if constexpr (GREG) {
+      if (gsel >= 0) {
+        d2 v = f.a[0];
+#pragma unroll
+        for (int i = 1; i < MB; ++i)
+          if (gsel == i) v = f.a[i];
+        gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, v.x, gacc, 0, 0, 0);
+        gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(v.y, v.y, gacc, 0, 0, 0);
+      }
+    }
   }
   __device__ __forceinline__ void compute(const char* __restrict__ st) {
     const int w = (threadIdx.x >> 6) - wo, l = threadIdx.x & 63;
@@ -410,8 +428,12 @@ __device__ __forceinline__ void gram_cand(int cand, int& q, int& br, int& bc) {
   }
 }
 
+// GREG (4-panel tiles, ntj >= 4): each diagonal Gram block is accumulated by a wave of the wave row that holds the
+// block's W rows, from the tile's own W fragments (GTile GREG) -- no LDS reads of its own; wave column (wr >> 1) & 1
+// of wave row wr, so at ntj = 4 the four chains of a workgroup sit on four SIMDs.  The straddling candidates (never
+// produced by the engine's 16-column block packing) keep the LDS form.  Same operands, same K order: bit-identical.
 template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1, bool ABLK = false, bool GRAM = true,
-          bool GITEM = false>
+          bool GITEM = false, bool GREG = false>
 static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
                                                               long m_pad, int ngroups, int ntj, int nsplit, int kchunk,
                                                               const int* __restrict__ prb, const int* __restrict__ pre,
@@ -420,7 +442,8 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
                                                               const int* __restrict__ stop_iter, double* __restrict__ Gpart,
                                                               long g_ld, long g_split, double* __restrict__ SWpart,
                                                               long sw_total) {
-  using T = GTile<64 * NPT, RQ, WR, WC, NBUF, ABLK>;
+  using T = GTile<64 * NPT, RQ, WR, WC, NBUF, ABLK, GREG>;
+  static_assert(!GREG || (WR == NPT && GPW == 1 && GRAM && !GITEM), "register Gram: one panel per wave row");
   constexpr int NCAND = 7 * NPT;
   __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES + 64];
   int* need = reinterpret_cast<int*>(smem + T::LDS_BYTES);
@@ -510,11 +533,21 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
     if (cand < NCAND) {
       int q, br, bc;
       gram_cand<NPT>(cand, q, br, bc);
-      my_need[x] = need[cand];
+      my_need[x] = (GREG && cand < 4 * NPT) ? 0 : need[cand];
       my_ra[x] = 64 * q + 16 * br;
       my_rb[x] = 64 * q + 16 * bc;
       gram = GRAM && !GITEM && (gram || my_need[x]);
     }
+  }
+  if constexpr (GREG) {
+    const int wr = w / WC, wc = w % WC;
+    int gs = -1;
+    if (wc == ((wr >> 1) & 1) % WC) {
+#pragma unroll
+      for (int br = 0; br < 4; ++br)
+        if ((4 * wr + br) % ntj == t && need[4 * wr + br]) gs = br;
+    }
+    tl.gsel = __builtin_amdgcn_readfirstlane(gs);
   }
   const double* P = W + (long)pg * 64 * NPT * m_pad + kbeg;
   tl.run(P, m_pad, Q, ldq, 0, kend - kbeg, smem, [&](const char* stg) {
@@ -541,23 +574,31 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
     for (int nb = 0; nb < T::NB; ++nb)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) out[(long)T::row_of(mb, reg) * g_ld + T::col_of(nb)] = tl.acc[mb][nb][reg];
-  if (gram) {
+  // the restart-diagonal entries of Gram block (rows ra .. ra + 15, columns rb .. rb + 15 of the tile)
+  auto put_gram = [&](int ra, int rb, const d4& v) {
     double* so = SWpart + (long)s * sw_total;
+    const int pnl = ra >> 6;
+    const ColInfo* cp = ci + (long)(NPT * pg + pnl) * PANEL;
 #pragma unroll
-    for (int x = 0; x < GPW; ++x) {
-      if (!my_need[x]) continue;
-      const int pnl = my_ra[x] >> 6;
-      const ColInfo* cp = ci + (long)(NPT * pg + pnl) * PANEL;
+    for (int reg = 0; reg < 4; ++reg) {
+      const int lr = (ra & 63) + g + 4 * reg;
+      const int lcn = (rb & 63) + fr;
+      const ColInfo cr = cp[lr];
+      if (cr.k == 0 || cr.lc0 != cp[lcn].lc0 || cp[lcn].k == 0) continue;
+      const int a = lr - cr.lc0, b = lcn - cr.lc0;
+      so[cr.sq_off + a * cr.k + b] = v[reg];
+      so[cr.sq_off + b * cr.k + a] = v[reg];
+    }
+  };
+  if (gram) {
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int lr = (my_ra[x] & 63) + g + 4 * reg;
-        const int lcn = (my_rb[x] & 63) + fr;
-        const ColInfo cr = cp[lr];
-        if (cr.k == 0 || cr.lc0 != cp[lcn].lc0 || cp[lcn].k == 0) continue;
-        const int a = lr - cr.lc0, b = lcn - cr.lc0;
-        so[cr.sq_off + a * cr.k + b] = gacc[x][reg];
-        so[cr.sq_off + b * cr.k + a] = gacc[x][reg];
-      }
+    for (int x = 0; x < GPW; ++x)
+      if (my_need[x]) put_gram(my_ra[x], my_rb[x], gacc[x]);
+  }
+  if constexpr (GREG) {
+    if (tl.gsel >= 0) {
+      const int rr = 64 * (w / WC) + 16 * tl.gsel;
+      put_gram(rr, rr, tl.gacc);
     }
   }
 }

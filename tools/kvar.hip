@@ -44,27 +44,42 @@ float timeit(F f, int reps) {
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 200, reps = argc > 2 ? atoi(argv[2]) : 10;
   const int m = 20000;
-  // packing of R restarts of every k = 10..2 into 64-column panels (k descending, sequential fill)
+  // packing of R restarts of every k = 10..2 as the engine packs them (engine.hip pack()): k descending, first fit
+  // into 16-column blocks (no restart across a block), four blocks to a 64-column panel
   std::vector<ColInfo> ci;
   std::vector<RestartInfo> ri;
   std::vector<int> pfirst;
-  int fill = PANEL, np = -1, sq = 0;
+  int np = -1, sq = 0;
   double fk = 0, fk2 = 0;   // sum of k, k^2
-  for (int k = 10; k >= 2; --k)
-    for (int r = 0; r < R; ++r) {
-      if (fill + k > PANEL) {
-        ++np;
-        fill = 0;
-        ci.resize((size_t)(np + 1) * PANEL, ColInfo{0, 0, 0, 0});
-        pfirst.push_back((int)ri.size());
+  {
+    std::vector<int> bfill;
+    std::vector<std::vector<std::pair<int, int>>> bmem;   // (k, first column in block)
+    for (int k = 10; k >= 2; --k)
+      for (int r = 0; r < R; ++r) {
+        size_t b = 0;
+        while (b < bfill.size() && bfill[b] + k > 16) ++b;
+        if (b == bfill.size()) {
+          bfill.push_back(0);
+          bmem.emplace_back();
+        }
+        bmem[b].push_back({k, bfill[b]});
+        bfill[b] += k;
       }
-      ri.push_back({np * PANEL + fill, k, (int)ri.size(), sq});
-      for (int a = 0; a < k; ++a) ci[(size_t)np * PANEL + fill + a] = ColInfo{sq, fill, k, (int)ri.size() - 1};
-      fk += k;
-      fk2 += (double)k * k;
-      sq += k * k;
-      fill += k;
+    const int nblocks = (int)bfill.size();
+    np = (nblocks + 3) / 4 - 1;
+    ci.assign((size_t)(np + 1) * PANEL, ColInfo{0, 0, 0, 0});
+    for (int b = 0; b < nblocks; ++b) {
+      if (b % 4 == 0) pfirst.push_back((int)ri.size());
+      for (auto [k, c0] : bmem[b]) {
+        const int col0 = 16 * b + c0;
+        ri.push_back({col0, k, (int)ri.size(), sq});
+        for (int a = 0; a < k; ++a) ci[(size_t)col0 + a] = ColInfo{sq, col0 % PANEL, k, (int)ri.size() - 1};
+        fk += k;
+        fk2 += (double)k * k;
+        sq += k * k;
+      }
     }
+  }
   const int live = np + 1, npanels = (live + 3) / 4 * 4;
   pfirst.push_back((int)ri.size());
   ci.resize((size_t)npanels * PANEL, ColInfo{0, 0, 0, 0});
@@ -144,6 +159,7 @@ int main(int argc, char** argv) {
 #define WA(...) hipLaunchKernelGGL((k_wta2<__VA_ARGS__>), dim3(nsplit * ng * ntj), dim3(512), 0, 0, W, Ablk, m_pad, ng, ntj, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, (long)sq)
     if (ntj >= 4) {
       report("k_wta2 big 4x128 nbuf3 (engine)", timeit([&] { WA(4, 128, 4, 2, 1, 3, 1, true); }, reps), flop);
+      report("  Gram from registers (GREG)", timeit([&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true); }, reps), flop);
       report("  no Gram chains", timeit([&] { WA(4, 128, 4, 2, 1, 3, 1, true, false); }, reps), flop);
       report("  nbuf 2", timeit([&] { WA(4, 128, 4, 2, 1, 2, 1, true); }, reps), flop);
     } else {
