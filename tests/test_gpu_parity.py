@@ -274,7 +274,9 @@ def test_ragged_shapes_vs_oracle(oracle, m, n, ks):
         assert np.all(r.H[j][:, 3] == 0.0)
 
 
-@pytest.mark.parametrize("n", [150, 100])   # 2 and 1 sample tiles of 128 (the Gram blocks spread differently)
+# 2 and 1 sample tiles of 128 (the Gram blocks spread differently); 4 and 16: the big tiles take their diagonal Gram
+# blocks from the W fragment registers (GTile GREG) while the other shapes stage them through LDS
+@pytest.mark.parametrize("n", [150, 100, 500, 2000])
 def test_tile_shapes_bit_identical(oracle, n):
     # every W^T A / A h^T tile shape the engine picks by grid size sums in the same canonical K order:
     # forcing each shape gives the same bits (so results never depend on how many restarts are live)
