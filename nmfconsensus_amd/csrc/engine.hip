@@ -1105,8 +1105,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->W[cur].as<double>(), e->SHP.as<double>(), e->colinfo.as<ColInfo>(),
                                e->colact.as<int>(), nblk, 4 * e->ngt);
           } else {
-            auto ka = ahtw_small ? k_ahtw4<0, GT / 2, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>
-                                 : k_ahtw4<0, GT, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>;
+            // the last K stage's second half is padding (samples >= n): the KHALF form skips it
+            const bool kh = AHTW_KSKIP && AHTW_NBUF == 2 && e->n_pad - n >= 8;
+            auto ka = ahtw_small ? (kh ? k_ahtw4<0, GT / 2, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE, AHTW_NBUF == 2>
+                                       : k_ahtw4<0, GT / 2, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>)
+                                 : (kh ? k_ahtw4<0, GT, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE, AHTW_NBUF == 2>
+                                       : k_ahtw4<0, GT, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>);
             hipLaunchKernelGGL(ka, dim3(grid_ahtw), dim3(256), 0, st, iter,
                                e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
                                e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), lp,

@@ -200,6 +200,7 @@ struct GTile {
       }
     }
   }
+  template <int NKK = 2>
   __device__ __forceinline__ void compute(const char* __restrict__ st) {
     const int w = (threadIdx.x >> 6) - wo, l = threadIdx.x & 63;
     const int wr = w / WC, wc = w % WC;
@@ -207,7 +208,7 @@ struct GTile {
     const char* sp = st + (wr * (RP / WR) + fr) * 128;
     const char* sq = st + RP * 128 + (wc * (RQ / WC) + fr) * 128;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < NKK; ++kk) {
       const int so = ((4 * kk + g) ^ (fr >> 1)) << 4;
       d2 a[MB], b[NB];
 #pragma unroll
@@ -245,9 +246,12 @@ struct GTile {
   // with `pre()`: runs right after the prologue's first DMA issue, so the workgroup's own setup loads
   // overlap the first stages' latency; returning false abandons the tile (the DMA is drained first)
   // and run returns false.  All waves must return the same answer.
-  template <int XL = 0, class Pre, class Extra, class AtLast>
+  // LASTKK (NBUF == 2) = 1: the last stage's second half (K positions 8..15) holds zeros in both operands (the K
+  // padding) and is skipped -- adding exact zeros to sums of non-negative products would change no bit.
+  template <int XL = 0, int LASTKK = 2, class Pre, class Extra, class AtLast>
   __device__ __forceinline__ bool run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
                                       int kbeg, int kend, char* __restrict__ smem, Pre pre, Extra extra, AtLast at_last) {
+    static_assert(LASTKK == 2 || NBUF == 2, "half last stage on the two-stage ring only");
     const int nst = (kend - kbeg) / BK2;
     bind(P, ldp, Q, ldq, kend);
     const uint32_t base = (uint32_t)(uintptr_t)smem;
@@ -260,22 +264,23 @@ struct GTile {
       wait_vmcnt<0>();
       step_barrier();
       if (nst == 1) at_last();
-      for (int s = 0; s < nst; ++s) {
+      for (int s = 0; s + 1 < nst; ++s) {
         const int b = s & 1;
-        if (s + 1 < nst) {
-          issue(base + (b ^ 1) * STAGE_BYTES, kbeg + (s + 1) * BK2);
-          if (s + 2 == nst) at_last();
-        }
+        issue(base + (b ^ 1) * STAGE_BYTES, kbeg + (s + 1) * BK2);
+        if (s + 2 == nst) at_last();
         const char* cur = smem + b * STAGE_BYTES;
         compute(cur);
         extra(cur);
-        if (s + 1 < nst) {
-          if (s + 2 == nst)
-            wait_vmcnt<XL>();
-          else
-            wait_vmcnt<0>();
-          step_barrier();
-        }
+        if (s + 2 == nst)
+          wait_vmcnt<XL>();
+        else
+          wait_vmcnt<0>();
+        step_barrier();
+      }
+      {   // last step
+        const char* cur = smem + ((nst - 1) & 1) * STAGE_BYTES;
+        compute<LASTKK>(cur);
+        extra(cur);
       }
       return true;
     }
@@ -1024,6 +1029,11 @@ static __global__ __launch_bounds__(NTH, MINW) void k_hupdate(int iter, int maxi
 #undef NMFC_HUPD_CASE
 }
 
+#ifndef NMFC_AHTW_KSKIP
+#define NMFC_AHTW_KSKIP 1
+#endif
+constexpr bool AHTW_KSKIP = NMFC_AHTW_KSKIP != 0;   // A h^T: skip the K-padding half of the last stage (KHALF)
+
 // ---------------------------------------------------------------------------------------------
 // Item map of the A h^T kernels: (panel, gene tile) from the XCD-contiguous item index.
 // ---------------------------------------------------------------------------------------------
@@ -1072,7 +1082,9 @@ template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = P
 static constexpr int ahtw4_lds() {
   return GTile<PR * NPT, GTG, NPT, WC, NBUF>::LDS_BYTES + (LATE ? 0 : NPT * PR * KMAX * 8);
 }
-template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4, bool LATE = false>
+// KHALF: the last K stage's second half is padding (n_pad - n >= 8, decided on the host): skipped.
+template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4, bool LATE = false,
+          bool KHALF = false>
 static __global__ __launch_bounds__(64 * NPT * WC,
                                     (163840 / ahtw4_lds<VARIANT, GTG, NBUF, NPT, PR, WC, LATE>()) * NPT * WC / 4 > 8
                                         ? 8
@@ -1122,7 +1134,7 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
   constexpr int NSH = NPT * PR * KMAX / 2 / NTH;
   static_assert(NSH * 2 * NTH == NPT * PR * KMAX, "h h^T rows split evenly over the threads");
   d2 shv[NSH];
-  const bool live = tl.template run<LATE ? 0 : TileW4::MB * TileW4::NB * 4>(
+  const bool live = tl.template run<LATE ? 0 : TileW4::MB * TileW4::NB * 4, KHALF ? 1 : 2>(
       H + (long)p0 * PR * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
       [&] {   // setup loads, independent of each other, overlapping the first stages' DMA
         cc = lane < PR ? ci[(long)p * PR + lane] : ColInfo{0, 0, 0, 0};
