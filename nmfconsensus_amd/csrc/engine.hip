@@ -149,9 +149,6 @@ constexpr int NARROW_NBUF = NMFC_NARROW_NBUF;      // LDS ring depth of the narr
 #ifndef NMFC_WTA_MID_MINW
 #define NMFC_WTA_MID_MINW 1
 #endif
-#ifndef NMFC_WTA_KVEND
-#define NMFC_WTA_KVEND 1
-#endif
 #ifndef NMFC_WTA_GREG
 #define NMFC_WTA_GREG 1
 #endif
@@ -1031,8 +1028,6 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       // workgroups (each would fetch a prologue stage before finding its panel idle) and no 1-panel W^T A ones
       const int lp = std::max(1, live_panels(pk));
       const int grid_ahtw = lp * ngt_ahtw;
-      // W^T A skips the zero genes m_k .. m_pad - 1 (K padding; exact zeros, so no bit changes)
-      const long m_k = NMFC_WTA_KVEND ? ((long)m + BK2 - 1) / BK2 * BK2 : e->m_pad;
       for (int c = 1; c <= chunk; ++c) {
         const int iter = it + c;
         {
@@ -1046,12 +1041,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
               hipLaunchKernelGGL((k_wta_narrow_lc<16, NARROW_NBUF, true>), dim3(e->nsplit * nblk * (ntq + 1)), dim3(128), 0,
                                  st, e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk,
                                  nblk, e->colinfo.as<ColInfo>(), e->Gpart.as<double>(), g_ld, g_split,
-                                 e->SWpart.as<double>(), sw_total, m_k);
+                                 e->SWpart.as<double>(), sw_total);
             else
               hipLaunchKernelGGL((k_wta_narrow<16, NARROW_NBUF, true>), dim3(e->nsplit * nblk * (ntq + 1)), dim3(64), 0, st,
                                  e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
                                  e->colinfo.as<ColInfo>(),
-                                 e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total, m_k);
+                                 e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
             auto kw = (ntj >= 4)   ? k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true, true, false, WTA_GREG>
@@ -1061,7 +1056,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->Ablk.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
                                e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
-                               sw_total, m_k);
+                               sw_total);
           } else if (wta_mid) {   // npanels is a multiple of WTA_NPT, so of 2
             const int ng = (lp + 1) / 2;
             auto kw = (ntj >= 2) ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW, true>
@@ -1070,13 +1065,13 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->Ablk.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
                                e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),
-                               sw_total, m_k);
+                               sw_total);
           } else if (!wta_tiny) {   // 1-panel tiles: the Gram blocks in 3 workgroups of their own per (chunk, panel)
             hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, GT_NBUF, 1, true, true, true>), dim3(e->nsplit * lp * (2 * ntj + 3)), dim3(256),
                                0, st, e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, lp, 2 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
-                               e->SWpart.as<double>(), sw_total, m_k);
+                               e->SWpart.as<double>(), sw_total);
           } else {   // few live panels: 1-panel x 32-sample tiles, two 16x16 blocks per wave (short chains);
                      // at most one live workgroup per CU: an 8-stage ring (more DMA in flight per CU, 96 KiB)
             auto kw = (long)e->nsplit * live_panels(pk) * 4 * ntj <= e->ncu ? k_wta2<1, 32, 4, 1, 1, 8, 1, true, true, true>
@@ -1085,7 +1080,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, lp, 4 * ntj, e->nsplit,
                                e->kchunk, e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(),
                                e->colinfo.as<ColInfo>(), e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split,
-                               e->SWpart.as<double>(), sw_total, m_k);
+                               e->SWpart.as<double>(), sw_total);
           }
         }
         {

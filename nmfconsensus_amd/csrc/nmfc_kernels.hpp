@@ -446,7 +446,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
                                                               const ColInfo* __restrict__ ci,
                                                               const int* __restrict__ stop_iter, double* __restrict__ Gpart,
                                                               long g_ld, long g_split, double* __restrict__ SWpart,
-                                                              long sw_total, long kvend) {
+                                                              long sw_total) {
   using T = GTile<64 * NPT, RQ, WR, WC, NBUF, ABLK, GREG>;
   static_assert(!GREG || (WR == NPT && GPW == 1 && GRAM && !GITEM), "register Gram: one panel per wave row");
   constexpr int NCAND = 7 * NPT;
@@ -475,7 +475,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
         if (!(c.k > 0 && c.lc0 < 16 * bc)) return;
       }
       const int kbeg = s * kchunk;
-      const int kend = (int)min((long)kbeg + kchunk, kvend);   // genes >= kvend: zero rows of W and A
+      const int kend = (int)min((long)kbeg + kchunk, m_pad);
       TG tg;
       tg.wo = w;
       tg.zero();
@@ -516,7 +516,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
   // ABLK: Acm is K-blocked over all ntj * RQ sample rows.  Both operands are rebased to the chunk start, so the
   // buffer offsets stay within one chunk (32-bit for any n_cols_pad up to 2^17).
   const int kbeg = s * kchunk;
-  const int kend = (int)min((long)kbeg + kchunk, kvend);   // genes >= kvend: zero rows of W and A
+  const int kend = (int)min((long)kbeg + kchunk, m_pad);
   const long ldq = ABLK ? (long)ntj * RQ : m_pad;
   const double* Q = ABLK ? Acm + (long)kbeg * ldq + (long)t * RQ * 16 : Acm + (long)t * RQ * m_pad + kbeg;
   T tl;
@@ -625,7 +625,7 @@ static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restri
                                                           long m_pad, int ntq, int nsplit, int kchunk, int nblk,
                                                           const ColInfo* __restrict__ ci, double* __restrict__ Gpart,
                                                           long g_ld, long g_split, double* __restrict__ SWpart,
-                                                          long sw_total, long kvend) {
+                                                          long sw_total) {
   using T = GTile<16, RQ, 1, 1, NBUF, ABLK>;
   using TG = GTile<16, 16, 1, 1, NBUF, false>;
   static_assert(TG::LDS_BYTES <= T::LDS_BYTES, "the Gram item's ring fits the tile's");
@@ -634,7 +634,7 @@ static __global__ __launch_bounds__(64) void k_wta_narrow(const double* __restri
   const int item = xcd_item(blockIdx.x, nsplit * nblk * nt);
   const int t = item % nt, bk = (item / nt) % nblk, s = item / (nt * nblk);
   const int kbeg = s * kchunk;
-  const int kend = (int)min((long)kbeg + kchunk, kvend);   // genes >= kvend: zero rows of W and A
+  const int kend = (int)min((long)kbeg + kchunk, m_pad);
   const int l = threadIdx.x, fr = l & 15, g = l >> 4;
   const double* Wb = W + (long)bk * 16 * m_pad + kbeg;
   if (t == ntq) {   // the Gram item
@@ -676,7 +676,7 @@ static __global__ __launch_bounds__(128) void k_wta_narrow_lc(const double* __re
                                                              long m_pad, int ntq, int nsplit, int kchunk, int nblk,
                                                              const ColInfo* __restrict__ ci, double* __restrict__ Gpart,
                                                              long g_ld, long g_split, double* __restrict__ SWpart,
-                                                             long sw_total, long kvend) {
+                                                             long sw_total) {
   static_assert(RQ == 16, "the Gram item shares the tile type: RQ = 16");
   using T = GTile<16, RQ, 1, 1, NBUF, ABLK>;
   __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES];
@@ -684,7 +684,7 @@ static __global__ __launch_bounds__(128) void k_wta_narrow_lc(const double* __re
   const int item = xcd_item(blockIdx.x, nsplit * nblk * nt);
   const int t = item % nt, bk = (item / nt) % nblk, s = item / (nt * nblk);
   const int kbeg = s * kchunk;
-  const int kend = (int)min((long)kbeg + kchunk, kvend);   // genes >= kvend: zero rows of W and A
+  const int kend = (int)min((long)kbeg + kchunk, m_pad);
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
   const bool gram = t == ntq;
   const double* Wb = W + (long)bk * 16 * m_pad + kbeg;

@@ -156,7 +156,7 @@ int main(int argc, char** argv) {
     const long n_cols_pad = (n + 127) / 128 * 128, g_ld = n_cols_pad, g_split = cols * g_ld;
     const int ntj = (int)(n_cols_pad / 128), ng = npanels / 4;
     printf("== W^T A, n = %ld (%d sample tiles)\n", n, ntj);
-#define WA(...) hipLaunchKernelGGL((k_wta2<__VA_ARGS__>), dim3(nsplit * ng * ntj), dim3(512), 0, 0, W, Ablk, m_pad, ng, ntj, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, (long)sq, (long)m_pad)
+#define WA(...) hipLaunchKernelGGL((k_wta2<__VA_ARGS__>), dim3(nsplit * ng * ntj), dim3(512), 0, 0, W, Ablk, m_pad, ng, ntj, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, (long)sq)
     if (ntj >= 4) {
       report("k_wta2 big 4x128 nbuf3 (engine)", timeit([&] { WA(4, 128, 4, 2, 1, 3, 1, true); }, reps), flop);
       report("  Gram from registers (GREG)", timeit([&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true); }, reps), flop);

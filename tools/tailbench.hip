@@ -162,9 +162,9 @@ int main(int argc, char** argv) {
     printf("\n== %d live panels (%d restarts), %d panels launched, useful %.3e flop per contraction\n", live, nlive,
            npanels, useful);
 #define WTA_ARGS                                                                                              \
-  W, Acm, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, sw_total, (long)m_pad
+  W, Acm, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, sw_total
 #define WTA_ARGS_B                                                                                            \
-  W, Ablk, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, sw_total, (long)m_pad
+  W, Ablk, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, sw_total
     auto report = [&](const char* name, float ms) {
       printf("  %-28s %8.4f ms  %6.1f TF\n", name, ms, useful / ms / 1e9);
     };
@@ -184,18 +184,18 @@ int main(int argc, char** argv) {
         report("GIT wta2 tiny 1x32 nbuf3", timeit([&] {
                  hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 3, 1, true, true, true>), dim3(nsplit * ng * ntg), dim3(256), 0, 0,
                                     W, Ablk, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split,
-                                    SWpart, sw_total, (long)m_pad);
+                                    SWpart, sw_total);
                }, reps));
         report("GIT wta2 tiny 1x32 nbuf8", timeit([&] {
                  hipLaunchKernelGGL((k_wta2<1, 32, 4, 1, 1, 8, 1, true, true, true>), dim3(nsplit * ng * ntg), dim3(256), 0, 0,
                                     W, Ablk, m_pad, ng, ntw, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split,
-                                    SWpart, sw_total, (long)m_pad);
+                                    SWpart, sw_total);
                }, reps));
         const int ntw2 = 2 * ntj, ntg2 = ntw2 + 3;
         report("GIT wta2 small 1x64 nbuf3", timeit([&] {
                  hipLaunchKernelGGL((k_wta2<1, 64, 2, 2, 1, 3, 1, true, true, true>), dim3(nsplit * ng * ntg2), dim3(256), 0, 0,
                                     W, Ablk, m_pad, ng, ntw2, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split,
-                                    SWpart, sw_total, (long)m_pad);
+                                    SWpart, sw_total);
                }, reps));
       }
       report("BLK wta2 tiny 1x32 nbuf3", timeit([&] {
@@ -252,27 +252,27 @@ int main(int argc, char** argv) {
       const int ntq = (int)(n_cols_pad / 16);
       report("wta narrow 16x16 nbuf4", timeit([&] {
                hipLaunchKernelGGL((k_wta_narrow<16, 4>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
-                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total, (long)m_pad);
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("wta narrow 16x16 nbuf8", timeit([&] {
                hipLaunchKernelGGL((k_wta_narrow<16, 8>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
-                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total, (long)m_pad);
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("BLK wta narrow 16x16 nbuf8", timeit([&] {
                hipLaunchKernelGGL((k_wta_narrow<16, 8, true>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Ablk, m_pad, ntq, nsplit,
-                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total, (long)m_pad);
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("BLK wta narrow 16x16 nbuf16", timeit([&] {
                hipLaunchKernelGGL((k_wta_narrow<16, 16, true>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Ablk, m_pad, ntq, nsplit,
-                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total, (long)m_pad);
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("wta narrow 16x16 nbuf16", timeit([&] {
                hipLaunchKernelGGL((k_wta_narrow<16, 16>), dim3(nsplit * (ntq + 1)), dim3(64), 0, 0, W, Acm, m_pad, ntq, nsplit,
-                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total, (long)m_pad);
+                                  kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
       report("wta narrow 16x32 nbuf6", timeit([&] {
                hipLaunchKernelGGL((k_wta_narrow<32, 6>), dim3(nsplit * (ntq / 2 + 1)), dim3(64), 0, 0, W, Acm, m_pad, ntq / 2,
-                                  nsplit, kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total, (long)m_pad);
+                                  nsplit, kchunk, 1, dci, Gpart, g_ld, g_split, SWpart, sw_total);
              }, reps));
     }
     report("hupdate", timeit([&] {
