@@ -149,6 +149,10 @@ constexpr int NARROW_NBUF = NMFC_NARROW_NBUF;      // LDS ring depth of the narr
 #ifndef NMFC_WTA_MID_MINW
 #define NMFC_WTA_MID_MINW 1
 #endif
+#ifndef NMFC_SMALL_NW8
+#define NMFC_SMALL_NW8 1
+#endif
+constexpr bool SMALL_NW8 = NMFC_SMALL_NW8 != 0;    // k_small_mu with eight waves where m_pad % 256 == 0
 #ifndef NMFC_WTA_GREG
 #define NMFC_WTA_GREG 1
 #endif
@@ -396,21 +400,21 @@ TileChoice choose_tiles(const nmfc_engine* e, int np_live, int ntj) {
   return tc;
 }
 
-// k_small_mu<GBW, JB> for this engine's shape (GBW = m_pad / 64 gene blocks per wave, JB = sample blocks)
-template <int GBW>
+// k_small_mu<GBW, JB, 0, NW> for this engine's shape (GBW = m_pad / (16 NW) gene blocks per wave, JB = sample blocks)
+template <int GBW, int NW>
 hipError_t launch_small_g(nmfc_engine* e, int nblocks, int maxiter, int stop_rule) {
   const int jb = (e->n + 15) / 16;
   auto args = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * SMALL_NW), 0, e->st, e->smallblk.as<SmallBlock>(),
+    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * NW), 0, e->st, e->smallblk.as<SmallBlock>(),
                        e->Arm.as<double>(), e->n_pad, e->Acm.as<double>(), e->m_pad, e->n, e->n_pad,
                        e->W[0].as<double>(), e->H[0].as<double>(), maxiter, stop_rule, e->stop_iter.as<int>(),
                        e->stop_reason.as<int>());
   };
   switch (jb) {
-    case 1: args(k_small_mu<GBW, 1>); break;
-    case 2: args(k_small_mu<GBW, 2>); break;
-    case 3: args(k_small_mu<GBW, 3>); break;
-    default: args(k_small_mu<GBW, 4>); break;
+    case 1: args(k_small_mu<GBW, 1, 0, NW>); break;
+    case 2: args(k_small_mu<GBW, 2, 0, NW>); break;
+    case 3: args(k_small_mu<GBW, 3, 0, NW>); break;
+    default: args(k_small_mu<GBW, 4, 0, NW>); break;
   }
   return hipGetLastError();
 }
@@ -486,16 +490,28 @@ int launch_small(nmfc_engine* e, int nblocks, int maxiter, int stop_rule) {
     set_err("k_small_mu: m_pad %ld / n_pad %ld unsupported for n = %d", e->m_pad, e->n_pad, e->n);
     return -1;
   }
-  switch (e->m_pad / 64) {
-    case 2: err = launch_small_g<2>(e, nblocks, maxiter, stop_rule); break;
-    case 4: err = launch_small_g<4>(e, nblocks, maxiter, stop_rule); break;
-    case 6: err = launch_small_g<6>(e, nblocks, maxiter, stop_rule); break;
-    case 8: err = launch_small_g<8>(e, nblocks, maxiter, stop_rule); break;
-    case 10: err = launch_small_g<10>(e, nblocks, maxiter, stop_rule); break;
-    case 12: err = launch_small_g<12>(e, nblocks, maxiter, stop_rule); break;
-    case 14: err = launch_small_g<14>(e, nblocks, maxiter, stop_rule); break;
-    case 16: err = launch_small_g<16>(e, nblocks, maxiter, stop_rule); break;
-    default: set_err("k_small_mu: m_pad %ld unsupported", e->m_pad); return -1;
+  // eight waves where the genes split into an even number of 16-gene blocks per wave (m_pad a multiple of 256),
+  // else four: a function of (m, n) only, so a job's bits stay independent of its batch
+  if (SMALL_NW8 && e->m_pad % 256 == 0) {
+    switch (e->m_pad / 128) {
+      case 2: err = launch_small_g<2, 8>(e, nblocks, maxiter, stop_rule); break;
+      case 4: err = launch_small_g<4, 8>(e, nblocks, maxiter, stop_rule); break;
+      case 6: err = launch_small_g<6, 8>(e, nblocks, maxiter, stop_rule); break;
+      case 8: err = launch_small_g<8, 8>(e, nblocks, maxiter, stop_rule); break;
+      default: set_err("k_small_mu: m_pad %ld unsupported", e->m_pad); return -1;
+    }
+  } else {
+    switch (e->m_pad / 64) {
+      case 2: err = launch_small_g<2, 4>(e, nblocks, maxiter, stop_rule); break;
+      case 4: err = launch_small_g<4, 4>(e, nblocks, maxiter, stop_rule); break;
+      case 6: err = launch_small_g<6, 4>(e, nblocks, maxiter, stop_rule); break;
+      case 8: err = launch_small_g<8, 4>(e, nblocks, maxiter, stop_rule); break;
+      case 10: err = launch_small_g<10, 4>(e, nblocks, maxiter, stop_rule); break;
+      case 12: err = launch_small_g<12, 4>(e, nblocks, maxiter, stop_rule); break;
+      case 14: err = launch_small_g<14, 4>(e, nblocks, maxiter, stop_rule); break;
+      case 16: err = launch_small_g<16, 4>(e, nblocks, maxiter, stop_rule); break;
+      default: set_err("k_small_mu: m_pad %ld unsupported", e->m_pad); return -1;
+    }
   }
   if (err != hipSuccess) {
     set_err("k_small_mu launch: %s", hipGetErrorString(err));

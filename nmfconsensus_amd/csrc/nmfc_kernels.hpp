@@ -1264,14 +1264,16 @@ struct SoloJob {
   int col0, k, rid, pad;
 };
 
-template <int JB>
+template <int JB, int NW = SMALL_NW>
 struct SmallSmem {
   double H[16][16 * JB];           // current H of the block (rows = columns c)
-  double Gp[SMALL_NW][16][16 * JB];
-  double SWp[SMALL_NW][16][16];
+  union {                          // G partials (G phase .. H update) and W0 transpositions (F/E phase) never overlap
+    double Gp[NW][16][16 * JB];
+    double T[NW][SMALL_GGMAX][16][17];   // per-wave W0 block transpositions (padded rows), SMALL_GG blocks
+  } u;
+  double SWp[NW][16][16];
   double SW[16][16];
   double S[16][16];                // h h^T, zero across restarts
-  double T[SMALL_NW][SMALL_GGMAX][16][17];   // per-wave W0 block transpositions (padded rows), SMALL_GG blocks
   double win[SMALL_MAXR][16][16];  // REF_COMPAT windows
   int cls[SMALL_MAXR][64];         // classes (REF_COMPAT: windows i < k; ARGMAX_STABLE: samples)
   int colr[16];                    // restart slot of each column (-1: padding)
@@ -1283,13 +1285,18 @@ struct SmallSmem {
 
 // SKIP != 0 only in tools/smallbench.hip (phase cost breakdown): bit 0 no G/W^T W, 1 no H update,
 // 2 no h h^T / stop rule, 3 no F/E/W update, 4 no E = W0 (h h^T), 5 W rule replaced by adds.
-template <int GBW, int JB, int SKIP = 0>
-static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
+// NW waves (4 or 8); GBW = m_pad / (16 NW) gene blocks per wave.  The wave partials are summed in wave order, so
+// the NW = 4 and NW = 8 forms differ in the last bits (each is a function of (m, n) only).
+template <int GBW, int JB, int SKIP = 0, int NW = SMALL_NW>
+static __global__ __launch_bounds__(64 * NW) void k_small_mu(
     const SmallBlock* __restrict__ blocks, const double* __restrict__ Arm, long ld_rm, const double* __restrict__ Acm,
     long m_pad, int n, long n_pad, double* __restrict__ W, double* __restrict__ H, int maxiter, int stop_rule,
     int* __restrict__ stop_iter, int* __restrict__ stop_reason) {
   constexpr int NP = 16 * JB;
-  __shared__ SmallSmem<JB> sm;
+  // prefetch distances: with eight waves (two per SIMD) the other wave covers part of the load latency, and the
+  // registers are half (256 per lane)
+  constexpr int PF = NW == 8 ? SMALL_PF / 2 : SMALL_PF, FPF = NW == 8 ? SMALL_FPF / 2 : SMALL_FPF;
+  __shared__ SmallSmem<JB, NW> sm;
   __shared__ SmallBlock blk;   // in LDS: indexed by restart slot at run time
   if (threadIdx.x == 0) blk = blocks[blockIdx.x];
   __syncthreads();
@@ -1304,8 +1311,8 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     sm.run[tid] = tid < nr;
     sm.unch[tid] = 0;
   }
-  for (int x = tid; x < SMALL_MAXR * 64; x += 64 * SMALL_NW) (&sm.cls[0][0])[x] = 0;   // nmf_mu.c:132
-  for (int x = tid; x < 16 * NP; x += 64 * SMALL_NW) {
+  for (int x = tid; x < SMALL_MAXR * 64; x += 64 * NW) (&sm.cls[0][0])[x] = 0;   // nmf_mu.c:132
+  for (int x = tid; x < 16 * NP; x += 64 * NW) {
     const int c = x / NP, j = x % NP;
     sm.H[c][j] = (j < n) ? H[(long)(blk.col0 + c) * n_pad + j] : 0.0;
   }
@@ -1330,15 +1337,15 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     d4 gacc[JB], sacc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int jb = 0; jb < JB; ++jb) gacc[jb] = (d4){0.0, 0.0, 0.0, 0.0};
-    // software-pipelined: the A rows of k-step t + SMALL_PF are loaded at step t into a register ring
+    // software-pipelined: the A rows of k-step t + PF are loaded at step t into a register ring
     // (the loads are L2 hits; issued just before their use they would expose the L2 latency every k-step)
     {
       constexpr int NKS = (SKIP & 1) ? 0 : 4 * GBW;
-      double pf[SMALL_PF][JB];
+      double pf[PF][JB];
       constexpr long LDR = (JB <= 2) ? 32 : 64;   // == ld_rm (n_pad = round_up(n, 32), n <= 16 JB; host-checked)
       const double* __restrict__ arow = ArmI + (long)(16 * w * GBW + lr) * LDR + lc;
 #pragma unroll
-      for (int t = 0; t < SMALL_PF; ++t)
+      for (int t = 0; t < PF; ++t)
         if (t < NKS) {
 #pragma unroll
           for (int jb = 0; jb < JB; ++jb) pf[t][jb] = arow[(long)(4 * t) * LDR + 16 * jb];
@@ -1348,35 +1355,38 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
         const int gb = t >> 2, r = t & 3;
         double av[JB];
 #pragma unroll
-        for (int jb = 0; jb < JB; ++jb) av[jb] = pf[t % SMALL_PF][jb];
-        if (t + SMALL_PF < NKS) {
+        for (int jb = 0; jb < JB; ++jb) av[jb] = pf[t % PF][jb];
+        if (t + PF < NKS) {
 #pragma unroll
-          for (int jb = 0; jb < JB; ++jb) pf[t % SMALL_PF][jb] = arow[(long)(4 * (t + SMALL_PF)) * LDR + 16 * jb];
+          for (int jb = 0; jb < JB; ++jb) pf[t % PF][jb] = arow[(long)(4 * (t + PF)) * LDR + 16 * jb];
         }
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb) gacc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(wr[gb][r], av[jb], gacc[jb], 0, 0, 0);
         sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(wr[gb][r], wr[gb][r], sacc, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);   // keep the issue order: prefetch distance SMALL_PF k-steps
+        __builtin_amdgcn_sched_barrier(0);   // keep the issue order: prefetch distance PF k-steps
       }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
-      for (int jb = 0; jb < JB; ++jb) sm.Gp[w][lr + 4 * r][16 * jb + lc] = gacc[jb][r];
+      for (int jb = 0; jb < JB; ++jb) sm.u.Gp[w][lr + 4 * r][16 * jb + lc] = gacc[jb][r];
       sm.SWp[w][lr + 4 * r][lc] = sacc[r];
     }
     __syncthreads();
-    {   // W^T W: wave partials in wave order
+    if (tid < 256) {   // W^T W: wave partials in wave order
       const int c = tid >> 4, d = tid & 15;
-      sm.SW[c][d] = ((sm.SWp[0][c][d] + sm.SWp[1][c][d]) + sm.SWp[2][c][d]) + sm.SWp[3][c][d];
+      double sw = sm.SWp[0][c][d];
+#pragma unroll
+      for (int v = 1; v < NW; ++v) sw += sm.SWp[v][c][d];
+      sm.SW[c][d] = sw;
       if (tid < SMALL_MAXR) sm.changed[tid] = 0;
     }
     __syncthreads();
     // ---- H update (nmf_mu.c:178, 184-191), new H kept in registers until every thread has read the old ----
-    double hn[(16 * NP + 64 * SMALL_NW - 1) / (64 * SMALL_NW)];
+    double hn[(16 * NP + 64 * NW - 1) / (64 * NW)];
 #pragma unroll
-    for (int u = 0; u < (16 * NP + 64 * SMALL_NW - 1) / (64 * SMALL_NW); ++u) {
-      const int x = tid + u * 64 * SMALL_NW;
+    for (int u = 0; u < (16 * NP + 64 * NW - 1) / (64 * NW); ++u) {
+      const int x = tid + u * 64 * NW;
       hn[u] = 0.0;
       if (x < 16 * NP) {
         const int c = x / NP, j = x % NP;
@@ -1384,7 +1394,9 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
         const double h0 = sm.H[c][j];
         hn[u] = h0;
         if (!(SKIP & 2) && q >= 0 && sm.run[q] && j < n) {
-          const double gsum = ((sm.Gp[0][c][j] + sm.Gp[1][c][j]) + sm.Gp[2][c][j]) + sm.Gp[3][c][j];
+          double gsum = sm.u.Gp[0][c][j];
+#pragma unroll
+          for (int v = 1; v < NW; ++v) gsum += sm.u.Gp[v][c][j];
           const int b0 = blk.lc0[q], kq = blk.k[q];
           double dsum = 0.0;
           for (int b = 0; b < kq; ++b) dsum = fma(sm.SW[c][b0 + b], sm.H[b0 + b][j], dsum);
@@ -1394,8 +1406,8 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     }
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < (16 * NP + 64 * SMALL_NW - 1) / (64 * SMALL_NW); ++u) {
-      const int x = tid + u * 64 * SMALL_NW;
+    for (int u = 0; u < (16 * NP + 64 * NW - 1) / (64 * NW); ++u) {
+      const int x = tid + u * 64 * NW;
       if (x < 16 * NP) sm.H[x / NP][x % NP] = hn[u];
     }
     __syncthreads();
@@ -1419,7 +1431,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     if (check) {
       if (stop_rule == STOP_REF_COMPAT) {
         // window i of restart q reads the flat k x n column-major buffer at [i*n, i*n + k)
-        for (int x = tid; x < nr * 16; x += 64 * SMALL_NW) {
+        for (int x = tid; x < nr * 16; x += 64 * NW) {
           const int q = x >> 4, i = x & 15, kq = blk.k[q];
           if (i >= kq || i >= n || !sm.run[q]) continue;
           int cl = 0;
@@ -1436,7 +1448,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
           }
         }
       } else if (stop_rule == STOP_ARGMAX_STABLE) {
-        for (int x = tid; x < nr * 64; x += 64 * SMALL_NW) {
+        for (int x = tid; x < nr * 64; x += 64 * NW) {
           const int q = x >> 6, j = x & 63;
           if (j >= n || !sm.run[q]) continue;
           int best = 0;
@@ -1462,13 +1474,13 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
     for (int q = 0; q < SMALL_MAXR; ++q) runmask |= (q < nr && sm.run[q]) ? (1 << q) : 0;
     const int qmine = sm.colr[lc];
     const bool upd = qmine >= 0 && ((runmask >> qmine) & 1);
-    constexpr int SMALL_GG = (GBW % 4 == 0) ? 4 : 2;
+    constexpr int SMALL_GG = (NW == 4 && GBW % 4 == 0) ? 4 : 2;   // eight waves: two chains per wave, two waves per SIMD
     constexpr int NQ = NP / 4;                                    // K steps of F (samples, 4 per step)
     constexpr int NFS = (SKIP & 8) ? 0 : (GBW / SMALL_GG) * NQ;   // (group, K step) pairs of this wave
-    constexpr long MP = 64L * GBW;                                // == m_pad (host-checked)
-    // the A columns of step t + SMALL_PF are loaded at step t into a register ring (rows >= n are in
+    constexpr long MP = 16L * NW * GBW;                           // == m_pad (host-checked)
+    // the A columns of step t + PF are loaded at step t into a register ring (rows >= n are in
     // bounds: Acm holds round_up(n, 128) columns, zero past n)
-    double fpf[SMALL_FPF][SMALL_GG];
+    double fpf[FPF][SMALL_GG];
     double hvq[NQ];   // the B operand of every F step (h^T rows), the same for every gene group
 #pragma unroll
     for (int q = 0; q < NQ; ++q) hvq[q] = sm.H[lc][4 * q + lr];
@@ -1479,7 +1491,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
       for (int i = 0; i < SMALL_GG; ++i) dst[i] = acol[(long)(4 * q) * MP + 16 * (g4 + i)];
     };
 #pragma unroll
-    for (int t = 0; t < SMALL_FPF; ++t)
+    for (int t = 0; t < FPF; ++t)
       if (t < NFS) f_load(t, fpf[t]);
     // GG gene blocks at a time: GG independent MFMA chains for F and for E (a single chain per block would
     // leave the matrix pipe waiting on the dependent-issue latency)
@@ -1492,15 +1504,15 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
         e[i] = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (!(SKIP & 16)) sm.T[w][i][lr + 4 * r][lc] = wr[g4 + i][r];
+          if (!(SKIP & 16)) sm.u.T[w][i][lr + 4 * r][lc] = wr[g4 + i][r];
       }
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const int t = (g4 / SMALL_GG) * NQ + q;
         double av[SMALL_GG];
 #pragma unroll
-        for (int i = 0; i < SMALL_GG; ++i) av[i] = fpf[t % SMALL_FPF][i];
-        if (t + SMALL_FPF < NFS) f_load(t + SMALL_FPF, fpf[t % SMALL_FPF]);
+        for (int i = 0; i < SMALL_GG; ++i) av[i] = fpf[t % FPF][i];
+        if (t + FPF < NFS) f_load(t + FPF, fpf[t % FPF]);
         // every step, also past n (zero rows of h^T add exact zeros): a data-dependent skip here makes the
         // compiler shuttle the accumulators between AGPRs and VGPRs around each step
 #pragma unroll
@@ -1513,7 +1525,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
         const double sv = sm.S[4 * q + lr][lc];
 #pragma unroll
         for (int i = 0; i < SMALL_GG; ++i)
-          e[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.T[w][i][lc][4 * q + lr], sv, e[i], 0, 0, 0);
+          e[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.u.T[w][i][lc][4 * q + lr], sv, e[i], 0, 0, 0);
       }
       __builtin_amdgcn_wave_barrier();
       if ((SKIP & 32) && upd) {
@@ -1561,7 +1573,7 @@ static __global__ __launch_bounds__(64 * SMALL_NW) void k_small_mu(
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       W[(long)(blk.col0 + lc) * m_pad + 16 * (w * GBW + gb) + 4 * r + lr] = wr[gb][r];
-  for (int x = tid; x < 16 * NP; x += 64 * SMALL_NW) {
+  for (int x = tid; x < 16 * NP; x += 64 * NW) {
     const int c = x / NP, j = x % NP;
     if (j < n) H[(long)(blk.col0 + c) * n_pad + j] = sm.H[c][j];
   }
