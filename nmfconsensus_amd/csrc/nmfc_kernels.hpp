@@ -1295,7 +1295,7 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
   constexpr int NP = 16 * JB;
   // prefetch distances: with eight waves (two per SIMD) the other wave covers part of the load latency, and the
   // registers are half (256 per lane)
-  constexpr int PF = NW == 8 ? SMALL_PF / 2 : SMALL_PF, FPF = NW == 8 ? SMALL_FPF / 2 : SMALL_FPF;
+  constexpr int PF = NW == 8 ? SMALL_PF / 2 : SMALL_PF, FPF = SMALL_FPF;   // 8 waves: PF 2 / 4 / 8 tied or slower, FPF 8 +1 %
   __shared__ SmallSmem<JB, NW> sm;
   __shared__ SmallBlock blk;   // in LDS: indexed by restart slot at run time
   if (threadIdx.x == 0) blk = blocks[blockIdx.x];
