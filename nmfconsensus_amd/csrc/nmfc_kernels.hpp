@@ -1411,7 +1411,7 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
       if (x < 16 * NP) sm.H[x / NP][x % NP] = hn[u];
     }
     __syncthreads();
-    // ---- h h^T (nmf_mu.c:200) by wave 0; stop rule (nmf_mu.c:253-282) by the other waves ----
+    // ---- h h^T (nmf_mu.c:200) by wave 0; stop rule (nmf_mu.c:253-282) by the other waves at the same time ----
     const bool check = !(SKIP & 4) && stop_rule != STOP_FIXED && iter > 1 && (iter % 2 == 0);
     if (w == 0 && !(SKIP & 4)) {
       d4 hh = (d4){0.0, 0.0, 0.0, 0.0};
@@ -1426,12 +1426,11 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
         const int qc = sm.colr[c];
         sm.S[c][d] = (qc >= 0 && qc == sm.colr[d]) ? hh[r] : 0.0;
       }
-    }
-    __syncthreads();
-    if (check) {
+    } else if (check) {   // concurrently with wave 0's h h^T chain: both only read the new H
+      const int t1 = tid - 64;
       if (stop_rule == STOP_REF_COMPAT) {
         // window i of restart q reads the flat k x n column-major buffer at [i*n, i*n + k)
-        for (int x = tid; x < nr * 16; x += 64 * NW) {
+        for (int x = t1; x < nr * 16; x += 64 * (NW - 1)) {
           const int q = x >> 4, i = x & 15, kq = blk.k[q];
           if (i >= kq || i >= n || !sm.run[q]) continue;
           int cl = 0;
@@ -1448,7 +1447,7 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
           }
         }
       } else if (stop_rule == STOP_ARGMAX_STABLE) {
-        for (int x = tid; x < nr * 64; x += 64 * NW) {
+        for (int x = t1; x < nr * 64; x += 64 * (NW - 1)) {
           const int q = x >> 6, j = x & 63;
           if (j >= n || !sm.run[q]) continue;
           int best = 0;
