@@ -1266,7 +1266,7 @@ struct SoloJob {
 
 template <int JB, int NW = SMALL_NW>
 struct SmallSmem {
-  double H[16][16 * JB];           // current H of the block (rows = columns c)
+  double H[2][16][16 * JB];        // H of the block (rows = columns c), double-buffered: the update writes the other one
   union {                          // G partials (G phase .. H update) and W0 transpositions (F/E phase) never overlap
     double Gp[NW][16][16 * JB];
     double T[NW][SMALL_GGMAX][16][17];   // per-wave W0 block transpositions (padded rows), SMALL_GG blocks
@@ -1314,7 +1314,7 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
   for (int x = tid; x < SMALL_MAXR * 64; x += 64 * NW) (&sm.cls[0][0])[x] = 0;   // nmf_mu.c:132
   for (int x = tid; x < 16 * NP; x += 64 * NW) {
     const int c = x / NP, j = x % NP;
-    sm.H[c][j] = (j < n) ? H[(long)(blk.col0 + c) * n_pad + j] : 0.0;
+    sm.H[0][c][j] = (j < n) ? H[(long)(blk.col0 + c) * n_pad + j] : 0.0;
   }
   double wr[GBW][4];
 #pragma unroll
@@ -1324,6 +1324,7 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
       wr[gb][r] = W[(long)(blk.col0 + lc) * m_pad + 16 * (w * GBW + gb) + 4 * r + lr];
   if (tid == 0) sm.nrun = nr;
   __syncthreads();
+  int hb = 0;   // sm.H[hb]: the current H
   for (int iter = 1; iter <= maxiter; ++iter) {
     // the operand base pointers are laundered every iteration: otherwise the compiler hoists the
     // per-k-step addresses of all 4*GBW k-steps out of the iteration loop (hundreds of registers)
@@ -1382,42 +1383,45 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
       if (tid < SMALL_MAXR) sm.changed[tid] = 0;
     }
     __syncthreads();
-    // ---- H update (nmf_mu.c:178, 184-191), new H kept in registers until every thread has read the old ----
-    double hn[(16 * NP + 64 * NW - 1) / (64 * NW)];
+    // ---- H update (nmf_mu.c:178, 184-191) from sm.H[hb] into sm.H[hb ^ 1] ----
+    // (the run flags for this iteration's W update are read here, before any thread can reach the bookkeeping below)
+    int runmask = 0;
 #pragma unroll
-    for (int u = 0; u < (16 * NP + 64 * NW - 1) / (64 * NW); ++u) {
-      const int x = tid + u * 64 * NW;
-      hn[u] = 0.0;
-      if (x < 16 * NP) {
-        const int c = x / NP, j = x % NP;
-        const int q = sm.colr[c];
-        const double h0 = sm.H[c][j];
-        hn[u] = h0;
-        if (!(SKIP & 2) && q >= 0 && sm.run[q] && j < n) {
-          double gsum = sm.u.Gp[0][c][j];
+    for (int q = 0; q < SMALL_MAXR; ++q) runmask |= (q < nr && sm.run[q]) ? (1 << q) : 0;
+    {
+      const double(*Ho)[NP] = sm.H[hb];
+      double(*Hn)[NP] = sm.H[hb ^ 1];
 #pragma unroll
-          for (int v = 1; v < NW; ++v) gsum += sm.u.Gp[v][c][j];
-          const int b0 = blk.lc0[q], kq = blk.k[q];
-          double dsum = 0.0;
-          for (int b = 0; b < kq; ++b) dsum = fma(sm.SW[c][b0 + b], sm.H[b0 + b][j], dsum);
-          hn[u] = mu_rule(h0, gsum, dsum);
+      for (int u = 0; u < (16 * NP + 64 * NW - 1) / (64 * NW); ++u) {
+        const int x = tid + u * 64 * NW;
+        if (x < 16 * NP) {
+          const int c = x / NP, j = x % NP;
+          const int q = sm.colr[c];
+          const double h0 = Ho[c][j];
+          double hv = h0;
+          if (!(SKIP & 2) && q >= 0 && ((runmask >> q) & 1) && j < n) {
+            double gsum = sm.u.Gp[0][c][j];
+#pragma unroll
+            for (int v = 1; v < NW; ++v) gsum += sm.u.Gp[v][c][j];
+            const int b0 = blk.lc0[q], kq = blk.k[q];
+            double dsum = 0.0;
+            for (int b = 0; b < kq; ++b) dsum = fma(sm.SW[c][b0 + b], Ho[b0 + b][j], dsum);
+            hv = mu_rule(h0, gsum, dsum);
+          }
+          Hn[c][j] = hv;
         }
       }
     }
+    hb ^= 1;
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < (16 * NP + 64 * NW - 1) / (64 * NW); ++u) {
-      const int x = tid + u * 64 * NW;
-      if (x < 16 * NP) sm.H[x / NP][x % NP] = hn[u];
-    }
-    __syncthreads();
+    const double(*Hc)[NP] = sm.H[hb];
     // ---- h h^T (nmf_mu.c:200) by wave 0; stop rule (nmf_mu.c:253-282) by the other waves at the same time ----
     const bool check = !(SKIP & 4) && stop_rule != STOP_FIXED && iter > 1 && (iter % 2 == 0);
     if (w == 0 && !(SKIP & 4)) {
       d4 hh = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int q = 0; q < NP / 4; ++q) {
-        const double hv = sm.H[lc][4 * q + lr];
+        const double hv = Hc[lc][4 * q + lr];
         hh = __builtin_amdgcn_mfma_f64_16x16x4f64(hv, hv, hh, 0, 0, 0);
       }
 #pragma unroll
@@ -1437,7 +1441,7 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
           double prev = 0.0;
           for (int jj = 0; jj < kq; ++jj) {
             const int f = i * n + jj, j = f / kq, a = f - j * kq;
-            const double v = sm.H[blk.lc0[q] + a][j];
+            const double v = Hc[blk.lc0[q] + a][j];
             if (jj > 0 && v > prev) cl = jj;
             prev = v;
           }
@@ -1451,9 +1455,9 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
           const int q = x >> 6, j = x & 63;
           if (j >= n || !sm.run[q]) continue;
           int best = 0;
-          double bv = sm.H[blk.lc0[q]][j];
+          double bv = Hc[blk.lc0[q]][j];
           for (int a = 1; a < blk.k[q]; ++a) {
-            const double v = sm.H[blk.lc0[q] + a][j];
+            const double v = Hc[blk.lc0[q] + a][j];
             if (v > bv) {
               bv = v;
               best = a;
@@ -1468,9 +1472,6 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
     }
     __syncthreads();
     // ---- F = A h^T, E = W0 (h h^T), W update (nmf_mu.c:198-216) ----
-    int runmask = 0;
-#pragma unroll
-    for (int q = 0; q < SMALL_MAXR; ++q) runmask |= (q < nr && sm.run[q]) ? (1 << q) : 0;
     const int qmine = sm.colr[lc];
     const bool upd = qmine >= 0 && ((runmask >> qmine) & 1);
     constexpr int SMALL_GG = (NW == 4 && GBW % 4 == 0) ? 4 : 2;   // eight waves: two chains per wave, two waves per SIMD
@@ -1482,7 +1483,7 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
     double fpf[FPF][SMALL_GG];
     double hvq[NQ];   // the B operand of every F step (h^T rows), the same for every gene group
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) hvq[q] = sm.H[lc][4 * q + lr];
+    for (int q = 0; q < NQ; ++q) hvq[q] = Hc[lc][4 * q + lr];
     const double* __restrict__ acol = AcmI + (long)lr * MP + 16 * w * GBW + lc;
     auto f_load = [&](int t, double* dst) {
       const int g4 = (t / NQ) * SMALL_GG, q = t % NQ;
@@ -1540,9 +1541,9 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // ---- stop bookkeeping (one thread, after every wave has applied its W rule), then every thread sees the
-    // new run flags ----
-    __syncthreads();
+    // ---- stop bookkeeping (one thread, right after its own W rule: every thread read this iteration's run flags
+    // before the barrier ahead of the F phase, and nothing reads the stop state until the barrier below), then
+    // every thread sees the new run flags ----
     if (tid == 0) {
       for (int q = 0; q < nr; ++q) {
         if (!sm.run[q]) continue;
@@ -1574,7 +1575,7 @@ static __global__ __launch_bounds__(64 * NW) void k_small_mu(
       W[(long)(blk.col0 + lc) * m_pad + 16 * (w * GBW + gb) + 4 * r + lr] = wr[gb][r];
   for (int x = tid; x < 16 * NP; x += 64 * NW) {
     const int c = x / NP, j = x % NP;
-    if (j < n) H[(long)(blk.col0 + c) * n_pad + j] = sm.H[c][j];
+    if (j < n) H[(long)(blk.col0 + c) * n_pad + j] = sm.H[hb][c][j];
   }
 }
 
