@@ -629,3 +629,24 @@ def test_solo_path_vs_oracle(oracle, m, n, k):
         assert bool(early.value) == (rule != 0 and ito < T), (T, rule)
         assert relfro(W, Wo) < TOL and relfro(H, Ho) < TOL, (m, n, k, T, relfro(W, Wo), relfro(H, Ho))
 
+
+
+@pytest.mark.parametrize("m,n", [(200, 40), (500, 24), (700, 33), (1000, 64), (300, 16)])
+def test_small_kernel_wave_forms_vs_oracle(oracle, m, n):
+    """k_small_mu runs eight waves where m_pad is a multiple of 256 (m = 200 / 500 / 700 / 1000: 2 / 4 / 6 / 8 gene
+    blocks per wave) and four otherwise (m = 300 -> m_pad 384): rank 5..8 restarts (not the solo kernel's) in batches
+    against the oracle -- fixed counts within 1e-9, and the REF_COMPAT exits exact."""
+    from nmfconsensus_amd.nmf import Engine
+    rng = np.random.default_rng(31 * m + n)
+    A = np.asfortranarray(rng.random((m, n)) * 2.0 + 0.05)
+    ks, R, T = [5, 6, 8], 2, 24
+    with Engine(A) as eng:
+        r = eng.run(ks, R, maxiter=T, seed=41, stop_rule=0, want_factors=True)
+        s = eng.run(ks, R, maxiter=10000, seed=41, stop_rule=1)
+    for j in range(len(ks) * R):
+        k = ks[j % len(ks)]
+        W0, H0 = oracle.init_restart(41 + j, m, n, k)
+        Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, T, 0)
+        assert relfro(r.W[j], Wo) < TOL and relfro(r.H[j], Ho) < TOL, (m, n, k)
+        _, _, it = oracle.nmf_mu(A, W0, H0, 10000, 1)
+        assert s.iters[j] == it, (m, n, k, j)
