@@ -1116,17 +1116,17 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         {
           TimedLaunch tl(e, KID_AHTW, iter % e->timing_stride == 0);
           if (narrow) {   // per live 16-column block: 16 rows x 32 genes, 2 waves
-            hipLaunchKernelGGL((k_ahtw4<0, GT / 4, GT_NBUF, 1, 16, 2>), dim3(4 * e->ngt * nblk), dim3(128), 0, st,
+            hipLaunchKernelGGL((k_ahtw4<GT / 4, GT_NBUF, 1, 16, 2>), dim3(4 * e->ngt * nblk), dim3(128), 0, st,
                                iter, e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad,
                                e->W[cur].as<double>(), e->SHP.as<double>(), e->colinfo.as<ColInfo>(),
                                e->colact.as<int>(), nblk, 4 * e->ngt);
           } else {
             // the last K stage's second half is padding (samples >= n): the KHALF form skips it
             const bool kh = AHTW_KSKIP && AHTW_NBUF == 2 && e->n_pad - n >= 8;
-            auto ka = ahtw_small ? (kh ? k_ahtw4<0, GT / 2, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE, AHTW_NBUF == 2>
-                                       : k_ahtw4<0, GT / 2, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>)
-                                 : (kh ? k_ahtw4<0, GT, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE, AHTW_NBUF == 2>
-                                       : k_ahtw4<0, GT, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>);
+            auto ka = ahtw_small ? (kh ? k_ahtw4<GT / 2, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE, AHTW_NBUF == 2>
+                                       : k_ahtw4<GT / 2, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>)
+                                 : (kh ? k_ahtw4<GT, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE, AHTW_NBUF == 2>
+                                       : k_ahtw4<GT, AHTW_NBUF, 1, PANEL, 4, AHTW_LATE>);
             hipLaunchKernelGGL(ka, dim3(grid_ahtw), dim3(256), 0, st, iter,
                                e->H[cur].as<double>(), e->n_pad, e->Arm.as<double>(), e->m_pad, e->W[cur].as<double>(),
                                e->SHP.as<double>(), e->colinfo.as<ColInfo>(), e->colact.as<int>(), lp,

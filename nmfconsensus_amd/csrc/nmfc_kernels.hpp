@@ -41,6 +41,21 @@ __device__ __forceinline__ double mu_rule(double old, double num, double den) {
   return t < 0.0 ? 0.0 : t;
 }
 
+// The wave's index in its workgroup as a wave-uniform (SGPR) value.  threadIdx.x >> 6 is uniform within a wave, but the
+// compiler does not know it: a buffer resource or a base pointer derived from it would be kept in VGPRs and every
+// buffer load / store through it wrapped in a readfirstlane "waterfall" loop (round 5: 64 such loops around k_ahtw4's
+// W0 loads and W stores).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// mu_rule without branches: the quotient and product are formed for every element and the zero cases selected after,
+// so a wave's rule is one straight instruction stream (no exec-mask branch per element).  The same bits as mu_rule for
+// every input: where mu_rule returns early, the select returns the same +0.0.
+__device__ __forceinline__ double mu_rule_sel(double old, double num, double den) {
+  const double q = num / (den + DIV_BY_ZERO_AVOIDANCE);
+  const double t = old * q;
+  return (old == 0.0 || num == 0.0 || t < 0.0) ? 0.0 : t;
+}
+
 // Workgroup id -> work item such that each XCD (blocks b, b+8, ... share one) receives a contiguous
 // range of items (bijective for any count; a speed choice only, never correctness).
 __device__ __forceinline__ int xcd_item(int b, int nblocks) {
@@ -146,7 +161,7 @@ struct GTile {
   }
   // piece i of this wave (the wave index is wave-uniform: read into an SGPR so M0 is scalar arithmetic)
   __device__ __forceinline__ void issue_piece(uint32_t buf, int k0, int i) const {
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) - wo;
+    const int w = wave_id() - wo;
     const uint32_t dst = buf + (uint32_t)(w + NW * i) * 1024u;
     if (i >= PPW_P)
       lds_dma16(rq, dst, voff[i], k0 * qkm);
@@ -464,7 +479,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
     using TG = GTile<16, 16, 1, 1, NBUF, false>;
     static_assert(3 * TG::LDS_BYTES <= T::LDS_BYTES, "three Gram rings fit the tile's");
     if (t >= ntj) {
-      const int w = threadIdx.x >> 6, l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
+      const int w = wave_id(), l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
       const int x = 3 * (t - ntj) + w;   // candidate: 4 diagonal, 3 straddling blocks
       if (w >= 3 || x >= 7) return;
       if (!panel_live(prb, pre, pg, ri, stop_iter, 0)) return;
@@ -685,7 +700,7 @@ static __global__ __launch_bounds__(128) void k_wta_narrow_lc(const double* __re
   const int t = item % nt, bk = (item / nt) % nblk, s = item / (nt * nblk);
   const int kbeg = s * kchunk;
   const int kend = (int)min((long)kbeg + kchunk, m_pad);
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
+  const int wave = wave_id(), l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
   const bool gram = t == ntq;
   const double* Wb = W + (long)bk * 16 * m_pad + kbeg;
   const long ldq = gram ? m_pad : (ABLK ? (long)ntq * RQ : m_pad);   // operands rebased to the chunk start
@@ -1078,23 +1093,22 @@ __device__ __forceinline__ void ahtw_map(int item, int npanels, int ngt, int& p,
 // LATE: the h h^T rows stay in registers through the K loop and are staged afterwards into a ring buffer
 // the last step no longer reads, and W0 is loaded after the loop: no LDS beyond the ring and no W0
 // registers live in the loop, so more workgroups fit a CU (their K loops cover each other's epilogues).
-template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4, bool LATE = false>
+template <int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4, bool LATE = false>
 static constexpr int ahtw4_lds() {
   return GTile<PR * NPT, GTG, NPT, WC, NBUF>::LDS_BYTES + (LATE ? 0 : NPT * PR * KMAX * 8);
 }
 // KHALF: the last K stage's second half is padding (n_pad - n >= 8, decided on the host): skipped.
-template <int VARIANT, int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4, bool LATE = false,
-          bool KHALF = false>
+template <int GTG = GT, int NBUF = GT_NBUF, int NPT = 1, int PR = PANEL, int WC = 4, bool LATE = false, bool KHALF = false>
 static __global__ __launch_bounds__(64 * NPT * WC,
-                                    (163840 / ahtw4_lds<VARIANT, GTG, NBUF, NPT, PR, WC, LATE>()) * NPT * WC / 4 > 8
+                                    (163840 / ahtw4_lds<GTG, NBUF, NPT, PR, WC, LATE>()) * NPT * WC / 4 > 8
                                         ? 8
-                                        : (163840 / ahtw4_lds<VARIANT, GTG, NBUF, NPT, PR, WC, LATE>()) * NPT * WC / 4)
+                                        : (163840 / ahtw4_lds<GTG, NBUF, NPT, PR, WC, LATE>()) * NPT * WC / 4)
 void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* __restrict__ Arm, long m_pad,
              double* __restrict__ W, const double* __restrict__ SHP, const ColInfo* __restrict__ ci,
              const int* __restrict__ colact, int npanels, int ngt) {
   using TileW4 = GTile<PR * NPT, GTG, NPT, WC, NBUF>;
   constexpr int AHTW4_SH = TileW4::LDS_BYTES;
-  constexpr int AHTW4_LDS = ahtw4_lds<VARIANT, GTG, NBUF, NPT, PR, WC, LATE>();
+  constexpr int AHTW4_LDS = ahtw4_lds<GTG, NBUF, NPT, PR, WC, LATE>();
   static_assert(AHTW4_LDS <= 163840, "LDS of one CU");
   static_assert(PR == PANEL || (PR == 16 && NPT == 1), "narrow tiles: one 16-column block");
   static_assert(!LATE || TileW4::STAGE_BYTES >= NPT * PR * KMAX * 8, "h h^T rows fit one ring stage");
@@ -1104,7 +1118,7 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
   int pp, gt;
   ahtw_map(xcd_item(blockIdx.x, (npanels / NPT) * ngt), npanels / NPT, ngt, pp, gt);
   const int p0 = pp * NPT;   // first panel of the tile
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w / WC, wc = w % WC;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), wr = w / WC, wc = w % WC;
   const int p = p0 + wr;     // this wave's panel
   ColInfo cc;
   uint64_t actmask = 0;
@@ -1123,9 +1137,7 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
     for (int reg = 0; reg < 4; ++reg)
 #pragma unroll
       for (int nb = 0; nb < TileW4::NB; ++nb)
-        w0[mb][nb][reg] = (VARIANT == 1 || VARIANT == 4)
-                              ? 1.0
-                              : __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rw, wvoff, woff(mb, reg, nb), 0));
+        w0[mb][nb][reg] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rw, wvoff, woff(mb, reg, nb), 0));
   };
   auto load_w0 = [&] {
 #pragma unroll
@@ -1134,7 +1146,11 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
   constexpr int NSH = NPT * PR * KMAX / 2 / NTH;
   static_assert(NSH * 2 * NTH == NPT * PR * KMAX, "h h^T rows split evenly over the threads");
   d2 shv[NSH];
-  const bool live = tl.template run<LATE ? 0 : TileW4::MB * TileW4::NB * 4, KHALF ? 1 : 2>(
+  // W0 blocks 0 and 1 go out with the last K stage's DMA (EARLY, the 2-stage LATE form): their latency is covered by
+  // the last step's MFMAs instead of opening the epilogue (round 5: +2 % at full load, tools/kvar.hip form EW)
+  constexpr bool EARLY = LATE && NBUF == 2 && TileW4::MB >= 2;
+  constexpr int XL = LATE ? (EARLY ? 2 * TileW4::NB * 4 : 0) : TileW4::MB * TileW4::NB * 4;
+  const bool live = tl.template run<XL, KHALF ? 1 : 2>(
       H + (long)p0 * PR * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
       [&] {   // setup loads, independent of each other, overlapping the first stages' DMA
         cc = lane < PR ? ci[(long)p * PR + lane] : ColInfo{0, 0, 0, 0};
@@ -1161,6 +1177,10 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
       [](const char*) {},
       [&] {
         if constexpr (!LATE) load_w0();
+        if constexpr (EARLY) {
+          load_w0_block(0);
+          load_w0_block(1);
+        }
       });
   if (!live) return;
   if constexpr (LATE) {
@@ -1171,10 +1191,17 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
     for (int j = 0; j < NSH; ++j) reinterpret_cast<d2*>(SHl)[tid + NTH * j] = shv[j];
     // W0 by 16-row blocks, one block ahead of the epilogue's block loop (block mb's E reads blocks
     // mb - 1 .. mb + 1 only), so at most three blocks are live at once
+    if constexpr (!EARLY) {
 #pragma unroll
-    for (int mb = 0; mb < (TileW4::MB < 2 ? TileW4::MB : 2); ++mb) load_w0_block(mb);
-    __syncthreads();
+      for (int mb = 0; mb < (TileW4::MB < 2 ? TileW4::MB : 2); ++mb) load_w0_block(mb);
+    }
   }
+  // Block-aligned restarts (the engine's 16-column block packing: no active restart crosses a 16-column block) take
+  // E over the four K steps of their own block, no shuffles for its K range; the K steps the restarts do not cover
+  // add exact zeros (0 x finite W0), so the bits are those of the general form, which stays for any other packing.
+  const bool cross = ((actmask >> lane) & 1) && ((cc.lc0 & (PR - 1)) >> 4) != (((cc.lc0 & (PR - 1)) + cc.k - 1) >> 4);
+  const bool aligned = __ballot(cross) == 0;   // wave-uniform
+  if constexpr (LATE) __syncthreads();
   if (actmask == 0) return;   // this wave's panel is idle (its partner panel is not)
   const double* SHw = SHl + (long)wr * PR * KMAX;
 #pragma unroll
@@ -1184,28 +1211,42 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
     }
     const int ra = 16 * mb + (lane & 15);
     const int alc = __shfl(cc.lc0, ra) & (PR - 1);   // tile-local (a restart never straddles a tile)
-    const int ak = (VARIANT == 2 || VARIANT == 4 || !((actmask >> ra) & 1)) ? 0 : __shfl(cc.k, ra);
-    int lo = ak ? alc : PANEL, hi = ak ? alc + ak : 0;
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) {
-      lo = min(lo, __shfl_xor(lo, off));
-      hi = max(hi, __shfl_xor(hi, off));
-    }
-    lo = __builtin_amdgcn_readfirstlane(lo);
-    hi = __builtin_amdgcn_readfirstlane(hi);
+    const int ak = ((actmask >> ra) & 1) ? __shfl(cc.k, ra) : 0;
     d4 e[TileW4::NB];
 #pragma unroll
     for (int nb = 0; nb < TileW4::NB; ++nb) e[nb] = d4{0.0, 0.0, 0.0, 0.0};
-    // K = the rows of the restarts touching block mb: within [16 mb - 15, 16 mb + 31) (k <= 16, restarts never
-    // leave the tile), i.e. K steps q in [4 mb - 4, 4 mb + 8)
+    if (aligned) {
+      double av[4];   // the block's four K steps' operands loaded ahead of the MFMA chain
 #pragma unroll
-    for (int q = (4 * mb - 4 > 0 ? 4 * mb - 4 : 0); q < (4 * mb + 8 < 4 * TileW4::MB ? 4 * mb + 8 : 4 * TileW4::MB); ++q) {
-      if (4 * q + 3 < lo || 4 * q >= hi) continue;   // wave-uniform
-      const int bb = 4 * q + (lane >> 4) - alc;
-      const double av = (bb >= 0 && bb < ak) ? SHw[ra * KMAX + bb] : 0.0;
+      for (int q = 0; q < 4; ++q) {
+        const int bb = 16 * mb + 4 * q + (lane >> 4) - alc;
+        av[q] = (bb >= 0 && bb < ak) ? SHw[ra * KMAX + bb] : 0.0;
+      }
 #pragma unroll
-      for (int nb = 0; nb < TileW4::NB; ++nb)
-        e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, w0[q >> 2][nb][q & 3], e[nb], 0, 0, 0);
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int nb = 0; nb < TileW4::NB; ++nb)
+          e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], w0[mb][nb][q], e[nb], 0, 0, 0);
+    } else {
+      int lo = ak ? alc : PANEL, hi = ak ? alc + ak : 0;
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off));
+        hi = max(hi, __shfl_xor(hi, off));
+      }
+      lo = __builtin_amdgcn_readfirstlane(lo);
+      hi = __builtin_amdgcn_readfirstlane(hi);
+      // K = the rows of the restarts touching block mb: within [16 mb - 15, 16 mb + 31) (k <= 16, restarts never
+      // leave the tile), i.e. K steps q in [4 mb - 4, 4 mb + 8)
+#pragma unroll
+      for (int q = (4 * mb - 4 > 0 ? 4 * mb - 4 : 0); q < (4 * mb + 8 < 4 * TileW4::MB ? 4 * mb + 8 : 4 * TileW4::MB); ++q) {
+        if (4 * q + 3 < lo || 4 * q >= hi) continue;   // wave-uniform
+        const int bb = 4 * q + (lane >> 4) - alc;
+        const double av = (bb >= 0 && bb < ak) ? SHw[ra * KMAX + bb] : 0.0;
+#pragma unroll
+        for (int nb = 0; nb < TileW4::NB; ++nb)
+          e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, w0[q >> 2][nb][q & 3], e[nb], 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
@@ -1213,9 +1254,8 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
       if (!((actmask >> c) & 1)) continue;
 #pragma unroll
       for (int nb = 0; nb < TileW4::NB; ++nb) {
-        const double v = VARIANT == 4 ? tl.acc[mb][nb][reg] : mu_rule(w0[mb][nb][reg], tl.acc[mb][nb][reg], e[nb][reg]);
-        if (VARIANT != 3 || v == (double)iter * 1.5e300)
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rw, wvoff, woff(mb, reg, nb), 0);
+        const double v = mu_rule_sel(w0[mb][nb][reg], tl.acc[mb][nb][reg], e[nb][reg]);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rw, wvoff, woff(mb, reg, nb), 0);
       }
     }
   }

@@ -61,9 +61,16 @@ def _dist_active(world: int) -> bool:
 
 
 def allreduce_counts(counts, group=None):
-    """SUM all-reduce of an int32 count tensor in place (torch tensor on the rank's device, or CPU for gloo)."""
+    """SUM all-reduce of an int32 count tensor in place (torch tensor on the rank's device, or CPU for gloo).
+    Under gloo (the CPU tests, several ranks sharing one GPU) a device tensor is staged through host memory: the
+    choice depends on the backend only, so every rank takes the same path.  RCCL ("nccl") reduces it in place."""
     import torch.distributed as dist
 
+    if counts.is_cuda and dist.get_backend(group) == "gloo":
+        host = counts.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        counts.copy_(host)
+        return counts
     dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
     return counts
 

@@ -2,13 +2,17 @@
 """Generates tests/golden/golden_c4.npz from the REFERENCE's own nmf_mu (TEST INFRASTRUCTURE ONLY).
 
 Run in the build container (needs /root/reference):
-    make -C oracle ref && python tests/golden/make_golden_c4.py [R] [procs] [T]
+    make -C oracle ref && python tests/golden/make_golden_c4.py [R] [procs] [T] [S]
+
+S (default 8) is the shard count whose uncovered shards get their first 14 jobs; 0 turns that off.
 
 BASELINE configs[3] (C4): synthetic 60000 x 2000 (nmfconsensus_amd.synthetic.planted_matrix; A is 960 MB
 and is NOT stored -- its SHA-256 is, and the GPU test refuses to compare against a different A),
 k = 2..15, the first R restarts of every k (default 2: jobs 0..27 of the C4 grid, which rank 0's shard of
 the 8-GPU job and the bench's per-GPU C4 shard both start with) plus the LAST T restarts of every k of the
-full 1000-restart grid (default 1: jobs 13986..13999, the end of rank 7's shard), seed 123, jobs in
+full 1000-restart grid (default 1: jobs 13986..13999, the end of rank 7's shard), plus (round 5) the first
+restart of every k inside each shard of the 8-GPU job that holds no golden job yet (`distributed.shard_range(14000,
+r, 8)`, r = 1..6: jobs 1750 r .. 1750 r + 13, 84 jobs), seed 123, jobs in
 expand.grid order (k fastest, nmf.r:63-68), job
 seed = seed + job_id - 1, init = the reference's generateMatrix(ran) after srand(job seed), REF_COMPAT
 exit (nmf_mu.c:253-282), maxiter 10000 (nmf.r:13).  Every job runs through oracle/_ref/libnmf_ref.so
@@ -18,8 +22,8 @@ single-threaded OpenBLAS, one process per core.
 Stored: job k, iterations, labels under both rules (argmax, nmf.r:128's order()[1]) as int8, the
 label margins (per job, the smallest relative gap between the winning and the runner-up entry of any
 sample column: a divergence at a tiny margin is a near-tie, not a bug), and the final H of the first
-restart of every k.  Counts and consensus are functions of the labels (nmf.r:140-143) and are
-rebuilt by the test.  A partial run (after an interruption) is resumable from the checkpoint in /tmp.
+restart of every k (and of every shard-head job of shard 3, which the rank-3 GPU test runs).  Counts and
+consensus are functions of the labels (nmf.r:140-143) and are rebuilt by the test.  A partial run (after an interruption) is resumable from the checkpoint in /tmp.
 """
 from __future__ import annotations
 
@@ -74,6 +78,7 @@ def main():
     R = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     procs = int(sys.argv[2]) if len(sys.argv) > 2 else min(7, os.cpu_count() or 1)
     T = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    S = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     from nmfconsensus_amd.synthetic import planted_matrix
     A = planted_matrix(M, N)
     a_sha = hashlib.sha256(np.ascontiguousarray(A).tobytes(order="F")).hexdigest()
@@ -81,6 +86,16 @@ def main():
     # (position in the golden, global job id, k, seed): restarts r = 1..R and r = R_TOTAL-T+1..R_TOTAL
     rs = list(range(1, R + 1)) + list(range(R_TOTAL - T + 1, R_TOTAL + 1))
     gids = [(r - 1) * len(KS) + i for r in rs for i in range(len(KS))]
+    n_first, n_last = R * len(KS), T * len(KS)
+    shard_heads = {}
+    if S > 0:
+        from nmfconsensus_amd.distributed import shard_range
+        for s in range(S):
+            jb, je = shard_range(R_TOTAL * len(KS), s, S)
+            if not any(jb <= g < je for g in gids):
+                heads = list(range(jb, min(jb + len(KS), je)))
+                shard_heads[s] = list(range(len(gids), len(gids) + len(heads)))
+                gids += heads
     jobs = [(p, KS[g % len(KS)], SEED + g) for p, g in enumerate(gids)]
     nj = len(jobs)
     iters = np.full(nj, -1, dtype=np.int32)
@@ -106,8 +121,9 @@ def main():
     print(f"C4 golden: {nj} jobs, {nj - len(todo)} from checkpoint, {procs} processes", file=sys.stderr)
     keep_jobs = set()
     for k in KS:   # the final H of the first and (with T > 0) the last job of every k
-        sel = [j for j, kk, _ in jobs if kk == k]
+        sel = [j for j, kk, _ in jobs[:n_first + n_last] if kk == k]
         keep_jobs.update([sel[0], sel[-1]])
+    keep_jobs.update(shard_heads.get(3, []))
     t0 = time.time()
     done = 0
 

@@ -6,12 +6,210 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <string>
 #include <vector>
 
 #include "../nmfconsensus_amd/csrc/nmfc_kernels.hpp"
 
 using namespace nmfc;
+
+// ---------------------------------------------------------------------------------------------------------------
+// k_ahtw_probe: a copy of the engine's k_ahtw4 in its full-load form (GTG = 128, 2-stage ring, one panel, LATE, KHALF),
+// with probe arms that the product kernel does not carry (round 5: moved out of nmfc_kernels.hpp):
+//   VARIANT 0  the engine's kernel (bit-identical output: checked in main against k_ahtw4)
+//   VARIANT 1  no W0 loads (W0 = 1.0)      2  no E (E = 0)      3  no W stores      4  no E, no rule (raw F stored)
+// epilogue forms (F flags):
+//   F_BL  the W rule without branches (selects; the same bits as mu_rule for every input)
+//   F_FD  ... and the divide as v_rcp_f64 + two Newton steps + the correction FMA, without v_div_scale / v_div_fmas /
+//         v_div_fixup (the same bits as IEEE division wherever those are identities: no operand or quotient near
+//         the denormal / overflow range) -- unguarded here, an upper bound for the guarded form
+//   F_E4  E over the four K steps of its own 16-row block always (no lo / hi shuffles; exact zeros elsewhere)
+//   F_EW  W0 blocks 0 and 1 issued with the last K stage's DMA (XL = 16 loads in flight across the last step)
+// STAMP: per-wave s_memtime stamps (diagnostic build; read its shares, never its length):
+//   [0] entry  [1] K loop done  [2] h h^T staged + first W0 blocks landed (barrier)  [3..6] block mb's stores issued
+//   [7] HW_ID  [8] XCC_ID
+// ---------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+constexpr int NSTAMP = 9;
+constexpr int F_BL = 1, F_FD = 2, F_E4 = 4, F_EW = 8;
+
+__device__ __forceinline__ double div_nr(double n, double d) {   // LLVM's f64 fdiv sequence without scale / fixup
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  const double q = n * r;
+  const double res = fma(-d, q, n);
+  return fma(res, r, q);
+}
+
+template <int FL>
+__device__ __forceinline__ double rule_form(double old, double num, double den) {
+  if constexpr (!(FL & F_BL)) return mu_rule(old, num, den);
+  const double dd = den + DIV_BY_ZERO_AVOIDANCE;
+  const double q = (FL & F_FD) ? div_nr(num, dd) : num / dd;
+  const double t = old * q;
+  return (old == 0.0 || num == 0.0 || t < 0.0) ? 0.0 : t;
+}
+
+template <int VARIANT, bool STAMP, bool KHALF, int FL = 0>
+static __global__ __launch_bounds__(256, 3) void k_ahtw_probe(int iter, const double* __restrict__ H, long n_pad,
+                                                              const double* __restrict__ Arm, long m_pad,
+                                                              double* __restrict__ W, const double* __restrict__ SHP,
+                                                              const ColInfo* __restrict__ ci, const int* __restrict__ colact,
+                                                              int npanels, int ngt, unsigned long long* __restrict__ st) {
+  constexpr int GTG = GT, NBUF = 2, NPT = 1, PR = PANEL, WC = 4;
+  using TileW4 = GTile<PR * NPT, GTG, NPT, WC, NBUF>;
+  constexpr int NTH = 64 * NPT * WC;
+  constexpr bool EW = (FL & F_EW) != 0;
+  __shared__ __attribute__((aligned(1024))) char smem[TileW4::LDS_BYTES];
+  unsigned long long ts[NSTAMP] = {};
+  if constexpr (STAMP) ts[0] = stamp();
+  int pp, gt;
+  ahtw_map(xcd_item(blockIdx.x, (npanels / NPT) * ngt), npanels / NPT, ngt, pp, gt);
+  const int p0 = pp * NPT;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), wr = w / WC, wc = w % WC;
+  const int p = p0 + wr;
+  ColInfo cc;
+  uint64_t actmask = 0;
+  TileW4 tl;
+  tl.zero();
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      W + (long)p * PR * m_pad + (long)gt * GTG + (GTG / WC) * wc, 0, (int)(PR * m_pad * 8), 0x00020000);
+  const int wvoff = (int)(((lane >> 4) * m_pad + (lane & 15)) * 8);
+  auto woff = [&](int mb, int reg, int nb) { return (int)(((16 * mb + 4 * reg) * m_pad + 16 * nb) * 8); };
+  double w0[TileW4::MB][TileW4::NB][4];
+  auto load_w0_block = [&](int mb) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+      for (int nb = 0; nb < TileW4::NB; ++nb)
+        w0[mb][nb][reg] = (VARIANT == 1 || VARIANT == 4)
+                              ? 1.0
+                              : __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rw, wvoff, woff(mb, reg, nb), 0));
+  };
+  constexpr int NSH = NPT * PR * KMAX / 2 / NTH;
+  d2 shv[NSH];
+  const bool live = tl.template run<EW ? 2 * TileW4::NB * 4 : 0, KHALF ? 1 : 2>(
+      H + (long)p0 * PR * n_pad, n_pad, Arm + (long)gt * GTG * n_pad, n_pad, 0, (int)n_pad, smem,
+      [&] {
+        cc = lane < PR ? ci[(long)p * PR + lane] : ColInfo{0, 0, 0, 0};
+        const int ca = lane < PR ? colact[(long)p0 * PR + lane] : -1;
+        const d2* src = reinterpret_cast<const d2*>(SHP + (long)p0 * PR * KMAX);
+#pragma unroll
+        for (int j = 0; j < NSH; ++j) shv[j] = src[tid + NTH * j];
+        actmask = __ballot(ca == iter);
+        return actmask != 0;
+      },
+      [](const char*) {},
+      [&] {
+        if constexpr (EW) {
+          load_w0_block(0);
+          load_w0_block(1);
+        }
+      });
+  if (!live) return;
+  if constexpr (STAMP) ts[1] = stamp();
+  const int nst = (int)n_pad / BK2;
+  double* SHl = reinterpret_cast<double*>(smem + ((nst - 2) % NBUF) * TileW4::STAGE_BYTES);
+#pragma unroll
+  for (int j = 0; j < NSH; ++j) reinterpret_cast<d2*>(SHl)[tid + NTH * j] = shv[j];
+  if constexpr (!EW) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) load_w0_block(mb);
+  }
+  // F_E4 holds only where no active restart crosses a 16-column block (the engine's block packing): wave-uniform
+  bool e4 = false;
+  if constexpr ((FL & F_E4) != 0) {
+    const bool cross = ((actmask >> lane) & 1) && cc.k > 0 && ((cc.lc0 & (PR - 1)) >> 4) != (((cc.lc0 & (PR - 1)) + cc.k - 1) >> 4);
+    e4 = __ballot(cross) == 0;
+  }
+  __syncthreads();
+  if constexpr (STAMP) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ts[2] = stamp();
+  }
+  const double* SHw = SHl + (long)wr * PR * KMAX;
+#pragma unroll
+  for (int mb = 0; mb < TileW4::MB; ++mb) {
+    if (mb + 2 < TileW4::MB) load_w0_block(mb + 2);
+    const int ra = 16 * mb + (lane & 15);
+    const int alc = __shfl(cc.lc0, ra) & (PR - 1);
+    const int ak = (VARIANT == 2 || VARIANT == 4 || !((actmask >> ra) & 1)) ? 0 : __shfl(cc.k, ra);
+    d4 e[TileW4::NB];
+#pragma unroll
+    for (int nb = 0; nb < TileW4::NB; ++nb) e[nb] = d4{0.0, 0.0, 0.0, 0.0};
+    if (e4) {
+      if (VARIANT != 2 && VARIANT != 4) {
+        double av[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int bb = 16 * mb + 4 * q + (lane >> 4) - alc;
+          av[q] = (bb >= 0 && bb < ak) ? SHw[ra * KMAX + bb] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int nb = 0; nb < TileW4::NB; ++nb)
+            e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], w0[mb][nb][q], e[nb], 0, 0, 0);
+      }
+    } else {
+      int lo = ak ? alc : PANEL, hi = ak ? alc + ak : 0;
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off));
+        hi = max(hi, __shfl_xor(hi, off));
+      }
+      lo = __builtin_amdgcn_readfirstlane(lo);
+      hi = __builtin_amdgcn_readfirstlane(hi);
+#pragma unroll
+      for (int q = (4 * mb - 4 > 0 ? 4 * mb - 4 : 0); q < (4 * mb + 8 < 4 * TileW4::MB ? 4 * mb + 8 : 4 * TileW4::MB); ++q) {
+        if (4 * q + 3 < lo || 4 * q >= hi) continue;
+        const int bb = 4 * q + (lane >> 4) - alc;
+        const double av = (bb >= 0 && bb < ak) ? SHw[ra * KMAX + bb] : 0.0;
+#pragma unroll
+        for (int nb = 0; nb < TileW4::NB; ++nb)
+          e[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, w0[q >> 2][nb][q & 3], e[nb], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int c = 16 * mb + (lane >> 4) + 4 * reg;
+      if (!((actmask >> c) & 1)) continue;
+#pragma unroll
+      for (int nb = 0; nb < TileW4::NB; ++nb) {
+        const double v = VARIANT == 4 ? tl.acc[mb][nb][reg] : rule_form<FL>(w0[mb][nb][reg], tl.acc[mb][nb][reg], e[nb][reg]);
+        if (VARIANT != 3 || v == (double)iter * 1.5e300)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rw, wvoff, woff(mb, reg, nb), 0);
+      }
+    }
+    if constexpr (STAMP) ts[3 + mb] = stamp();
+  }
+  if constexpr (STAMP) {
+    ts[7] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+    ts[8] = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));   // HW_REG_XCC_ID
+    if (lane < NSTAMP) {
+      unsigned long long v = ts[0];
+#pragma unroll
+      for (int i = 1; i < NSTAMP; ++i)
+        if (lane == i) v = ts[i];
+      st[((long)blockIdx.x * 4 + w) * NSTAMP + lane] = v;
+    }
+  }
+}
 
 #define CK(x)                                                                                 \
   do {                                                                                        \
@@ -89,13 +287,16 @@ int main(int argc, char** argv) {
   const int nall = (int)ri.size();
   printf("kvar: R=%d, %d restarts in %d panels (%d launched), %d gene tiles\n", R, nall, live, npanels, ngt);
   const long nmax = 2048;
-  double *W, *Hh, *Arm, *Ablk, *SHP, *Gpart, *SWpart;
+  double *W, *Wb, *Hh, *Arm, *Ablk, *SHP, *Gpart, *SWpart;
+  unsigned long long* dstamp;
   int *colact, *dprb, *dpre, *stop;
   ColInfo* dci;
   RestartInfo* dri;
   const long n_cols_max = nmax;
   const int kchunk = 2048, nsplit = (int)((m_pad + kchunk - 1) / kchunk);
   CK(hipMalloc(&W, sizeof(double) * cols * m_pad));
+  CK(hipMalloc(&Wb, sizeof(double) * cols * m_pad));
+  CK(hipMalloc(&dstamp, sizeof(unsigned long long) * (size_t)(np + 1) * (m_pad / GT) * 4 * NSTAMP));
   CK(hipMalloc(&Hh, sizeof(double) * cols * nmax));
   CK(hipMalloc(&Arm, sizeof(double) * m_pad * nmax));
   CK(hipMalloc(&Ablk, sizeof(double) * m_pad * n_cols_max));
@@ -138,21 +339,102 @@ int main(int argc, char** argv) {
     const long n_pad = (n + BK - 1) / BK * BK;
     const double flop = 2.0 * m * n * fk + 2.0 * m * fk2;   // one contraction (+ its k^2 part), every restart
     printf("\n== A h^T, n = %ld (n_pad %ld)\n", n, n_pad);
-#define AH(V) \
-  hipLaunchKernelGGL((k_ahtw4<V, GT, 2, 1, PANEL, 4, true>), dim3(live * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm, m_pad, W, SHP, dci, colact, live, ngt)
-    report("k_ahtw4 128 LATE (engine)", timeit([&] { AH(0); }, reps), flop);
-    report("  V1 no W0 loads", timeit([&] { AH(1); }, reps), flop);
-    report("  V2 no E", timeit([&] { AH(2); }, reps), flop);
-    report("  V3 no W stores", timeit([&] { AH(3); }, reps), flop);
-    report("  V4 no E, no rule (raw F stored)", timeit([&] { AH(4); }, reps), flop);
-    report("k_ahtw4 128 nbuf3 (not LATE, 2/CU)", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, GT, 3, 1, PANEL, 4, false>), dim3(live * ngt), dim3(256), 0, 0, 1, Hh, n_pad, Arm,
-                                m_pad, W, SHP, dci, colact, live, ngt);
-           }, reps), flop);
-    report("k_ahtw4 2x128 nbuf3 (8 waves)", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, GT, 3, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, 1, Hh, n_pad, Arm, m_pad, W,
-                                SHP, dci, colact, npanels, ngt);
-           }, reps), flop);
+#define AH_ARGS Hh, n_pad, Arm, m_pad, W, SHP, dci, colact, live, ngt
+#define AP(V, S) hipLaunchKernelGGL((k_ahtw_probe<V, S, true>), dim3(live * ngt), dim3(256), 0, 0, 1, AH_ARGS, dstamp)
+#define AF(FLG) hipLaunchKernelGGL((k_ahtw_probe<0, false, true, FLG>), dim3(live * ngt), dim3(256), 0, 0, 1, AH_ARGS, dstamp)
+    std::vector<std::pair<std::string, std::function<void()>>> arms = {
+        {"k_ahtw4 128 LATE KHALF (engine)", [&] {
+           hipLaunchKernelGGL((k_ahtw4<GT, 2, 1, PANEL, 4, true, true>), dim3(live * ngt), dim3(256), 0, 0, 1, AH_ARGS);
+         }},
+        {"  probe V0 (= engine)", [&] { AP(0, false); }},
+        {"  V1 no W0 loads", [&] { AP(1, false); }},
+        {"  V2 no E", [&] { AP(2, false); }},
+        {"  V3 no W stores", [&] { AP(3, false); }},
+        {"  V4 no E, no rule (raw F stored)", [&] { AP(4, false); }},
+        {"  form BL (branch-free rule)", [&] { AF(F_BL); }},
+        {"  form BL+FD (fast divide, unguarded)", [&] { AF(F_BL | F_FD); }},
+        {"  form E4 (4 K steps, no lo/hi)", [&] { AF(F_E4); }},
+        {"  form EW (W0 0,1 with the last DMA)", [&] { AF(F_EW); }},
+        {"  form BL+E4", [&] { AF(F_BL | F_E4); }},
+        {"  form BL+FD+E4", [&] { AF(F_BL | F_FD | F_E4); }},
+        {"  form BL+FD+E4+EW", [&] { AF(F_BL | F_FD | F_E4 | F_EW); }},
+    };
+    {   // every arm that keeps the arithmetic (V0 and the forms): one launch from the same W as one engine launch
+      std::vector<double> x((size_t)cols * m_pad), y((size_t)cols * m_pad);
+      for (auto& [name, launch] : arms) {
+        if (name.find("V0") == std::string::npos && name.find("form") == std::string::npos) continue;
+        CK(hipMemcpy(Wb, W, sizeof(double) * cols * m_pad, hipMemcpyDeviceToDevice));
+        arms[0].second();
+        std::swap(W, Wb);
+        launch();
+        std::swap(W, Wb);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(x.data(), W, sizeof(double) * x.size(), hipMemcpyDeviceToHost));
+        CK(hipMemcpy(y.data(), Wb, sizeof(double) * y.size(), hipMemcpyDeviceToHost));
+        const bool eq = memcmp(x.data(), y.data(), sizeof(double) * x.size()) == 0;
+        printf("  %-44s output %s the engine's\n", name.c_str(), eq ? "bit-identical to" : "DIFFERS FROM");
+      }
+    }
+    {   // interleaved rounds (the chip's clock drifts with load and temperature): median and min per arm
+      for (int i = 0; i < 200; ++i) arms[0].second();   // ~1 s of load before the first round
+      CK(hipDeviceSynchronize());
+      const int rounds = 7;
+      std::vector<std::vector<float>> t(arms.size());
+      for (int r = 0; r < rounds; ++r)
+        for (size_t q = 0; q < arms.size(); ++q) t[q].push_back(timeit(arms[q].second, reps));
+      printf("  %d interleaved rounds of %d launches per arm: median (min)\n", rounds, reps);
+      for (size_t q = 0; q < arms.size(); ++q) {
+        std::vector<float> v = t[q];
+        std::sort(v.begin(), v.end());
+        printf("  %-44s %8.4f ms  %6.2f TF   (%6.2f)\n", arms[q].first.c_str(), v[v.size() / 2], flop / v[v.size() / 2] / 1e9,
+               flop / v[0] / 1e9);
+      }
+    }
+    {   // stamped probe: phase shares per wave and, per CU, how many of its workgroups are in their K loop
+      const long nw = (long)live * ngt * 4;
+      AP(0, true);
+      AP(0, true);
+      CK(hipDeviceSynchronize());
+      std::vector<unsigned long long> t((size_t)nw * NSTAMP);
+      CK(hipMemcpy(t.data(), dstamp, sizeof(unsigned long long) * t.size(), hipMemcpyDeviceToHost));
+      double sum[8] = {};
+      long cnt = 0;
+      std::map<long, std::vector<std::pair<unsigned long long, int>>> ev;   // CU -> (time, +1/-1 K loop; +2/-2 epilogue)
+      for (long i = 0; i < nw; ++i) {
+        const unsigned long long* r = &t[(size_t)i * NSTAMP];
+        if (r[6] == 0) continue;   // idle wave
+        for (int j = 1; j <= 6; ++j) sum[j] += (double)(r[j] - r[j - 1]);
+        sum[7] += (double)(r[6] - r[0]);
+        ++cnt;
+        if (i % 4 == 0) {
+          const long cu = ((long)(r[8] & 0xf) << 16) | (long)((r[7] >> 8) & 0xff);
+          ev[cu].push_back({r[0], 1});
+          ev[cu].push_back({r[1], -1});
+          ev[cu].push_back({r[1], 2});
+          ev[cu].push_back({r[6], -2});
+        }
+      }
+      const char* nm[8] = {"", "K loop", "hhT stage + W0 blocks 0,1 landed", "block 0 (E, rule, stores)", "block 1", "block 2",
+                           "block 3", "whole tile"};
+      printf("  stamped probe: %ld waves; mean cycles per wave-tile:\n", cnt);
+      for (int j = 1; j <= 7; ++j) printf("    %-36s %9.0f  (%5.1f %%)\n", nm[j], sum[j] / cnt, 100.0 * sum[j] / sum[7]);
+      // per CU: time with 0 / 1 / 2 / 3 workgroups in their K loop (between its first start and last end)
+      double occ[5] = {}, epi_k0 = 0, tot = 0;
+      for (auto& [cu, v] : ev) {
+        std::sort(v.begin(), v.end());
+        int nk = 0, ne = 0;
+        for (size_t q = 0; q + 1 < v.size(); ++q) {
+          if (v[q].second == 1 || v[q].second == -1) nk += v[q].second; else ne += v[q].second / 2;
+          const double dt = (double)(v[q + 1].first - v[q].first);
+          occ[nk < 4 ? nk : 4] += dt;
+          if (nk == 0 && ne > 0) epi_k0 += dt;
+          tot += dt;
+        }
+      }
+      printf("  per CU, share of time with 0/1/2/3 workgroups in their K loop: %.1f / %.1f / %.1f / %.1f %% "
+             "(%.1f %% with none in a K loop and one in its epilogue); %zu CUs\n", 100 * occ[0] / tot, 100 * occ[1] / tot,
+             100 * occ[2] / tot, 100 * occ[3] / tot, 100 * epi_k0 / tot, ev.size());
+    }
     const long n_cols_pad = (n + 127) / 128 * 128, g_ld = n_cols_pad, g_split = cols * g_ld;
     const int ntj = (int)(n_cols_pad / 128), ng = npanels / 4;
     printf("== W^T A, n = %ld (%d sample tiles)\n", n, ntj);

@@ -283,51 +283,51 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(colact, ca.data(), sizeof(int) * ca.size(), hipMemcpyHostToDevice));   // hupdate stamped iter 1
 #define AHTW_ARGS(NGT) 1, Hh, n_pad, Arm, m_pad, W, SHP, dci, colact, npanels, NGT
     report("ahtw4 64 nbuf3", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, 64, 3>), dim3(npanels * 2 * ngt), dim3(256), 0, 0, AHTW_ARGS(2 * ngt));
+             hipLaunchKernelGGL((k_ahtw4<64, 3>), dim3(npanels * 2 * ngt), dim3(256), 0, 0, AHTW_ARGS(2 * ngt));
            }, reps));
     report("ahtw4 64 nbuf4", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, 64, 4>), dim3(npanels * 2 * ngt), dim3(256), 0, 0, AHTW_ARGS(2 * ngt));
+             hipLaunchKernelGGL((k_ahtw4<64, 4>), dim3(npanels * 2 * ngt), dim3(256), 0, 0, AHTW_ARGS(2 * ngt));
            }, reps));
     report("ahtw4 64 nbuf6", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, 64, 6>), dim3(npanels * 2 * ngt), dim3(256), 0, 0, AHTW_ARGS(2 * ngt));
+             hipLaunchKernelGGL((k_ahtw4<64, 6>), dim3(npanels * 2 * ngt), dim3(256), 0, 0, AHTW_ARGS(2 * ngt));
            }, reps));
     report("ahtw4 128 nbuf3", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, 128, 3>), dim3(npanels * ngt), dim3(256), 0, 0, AHTW_ARGS(ngt));
+             hipLaunchKernelGGL((k_ahtw4<128, 3>), dim3(npanels * ngt), dim3(256), 0, 0, AHTW_ARGS(ngt));
            }, reps));
     report("ahtw4 128 nbuf4", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, 128, 4>), dim3(npanels * ngt), dim3(256), 0, 0, AHTW_ARGS(ngt));
+             hipLaunchKernelGGL((k_ahtw4<128, 4>), dim3(npanels * ngt), dim3(256), 0, 0, AHTW_ARGS(ngt));
            }, reps));
     if (only && ri[nlive - 1].col0 + ri[nlive - 1].k <= 16) {
       report("ahtw narrow 16x64 (2w)", timeit([&] {
-               hipLaunchKernelGGL((k_ahtw4<0, 64, 3, 1, 16, 2>), dim3(2 * ngt), dim3(128), 0, 0, 1, Hh, n_pad, Arm,
+               hipLaunchKernelGGL((k_ahtw4<64, 3, 1, 16, 2>), dim3(2 * ngt), dim3(128), 0, 0, 1, Hh, n_pad, Arm,
                                   m_pad, W, SHP, dci, colact, 1, 2 * ngt);
              }, reps));
       report("ahtw narrow 16x32 (2w)", timeit([&] {
-               hipLaunchKernelGGL((k_ahtw4<0, 32, 3, 1, 16, 2>), dim3(4 * ngt), dim3(128), 0, 0, 1, Hh, n_pad, Arm,
+               hipLaunchKernelGGL((k_ahtw4<32, 3, 1, 16, 2>), dim3(4 * ngt), dim3(128), 0, 0, 1, Hh, n_pad, Arm,
                                   m_pad, W, SHP, dci, colact, 1, 4 * ngt);
              }, reps));
       report("ahtw narrow 16x128 (2w)", timeit([&] {
-               hipLaunchKernelGGL((k_ahtw4<0, 128, 3, 1, 16, 2>), dim3(ngt), dim3(128), 0, 0, 1, Hh, n_pad, Arm,
+               hipLaunchKernelGGL((k_ahtw4<128, 3, 1, 16, 2>), dim3(ngt), dim3(128), 0, 0, 1, Hh, n_pad, Arm,
                                   m_pad, W, SHP, dci, colact, 1, ngt);
              }, reps));
     }
     report("ahtw4 2x128 nbuf3 (8w)", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, 128, 3, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
+             hipLaunchKernelGGL((k_ahtw4<128, 3, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
            }, reps));
     report("ahtw4 2x128 nbuf4 (8w)", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, 128, 4, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
+             hipLaunchKernelGGL((k_ahtw4<128, 4, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
            }, reps));
     report("ahtw4 2x64 nbuf3 (8w)", timeit([&] {
-             hipLaunchKernelGGL((k_ahtw4<0, 64, 3, 2>), dim3(npanels / 2 * 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(2 * ngt));
+             hipLaunchKernelGGL((k_ahtw4<64, 3, 2>), dim3(npanels / 2 * 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(2 * ngt));
            }, reps));
     {   // bit-identity of the 2-panel tile against the 1-panel tile (same canonical K order)
       const size_t nw = (size_t)npanels * PANEL * m_pad;
       std::vector<double> w1(nw), w2(nw), w0(nw);
       CK(hipMemcpy(w0.data(), W, nw * 8, hipMemcpyDeviceToHost));
-      hipLaunchKernelGGL((k_ahtw4<0, 128, 3>), dim3(npanels * ngt), dim3(256), 0, 0, AHTW_ARGS(ngt));
+      hipLaunchKernelGGL((k_ahtw4<128, 3>), dim3(npanels * ngt), dim3(256), 0, 0, AHTW_ARGS(ngt));
       CK(hipMemcpy(w1.data(), W, nw * 8, hipMemcpyDeviceToHost));
       CK(hipMemcpy(W, w0.data(), nw * 8, hipMemcpyHostToDevice));
-      hipLaunchKernelGGL((k_ahtw4<0, 128, 3, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
+      hipLaunchKernelGGL((k_ahtw4<128, 3, 2>), dim3(npanels / 2 * ngt), dim3(512), 0, 0, AHTW_ARGS(ngt));
       CK(hipMemcpy(w2.data(), W, nw * 8, hipMemcpyDeviceToHost));
       CK(hipMemcpy(W, w0.data(), nw * 8, hipMemcpyHostToDevice));
       size_t diff = 0, changed = 0;
