@@ -7,10 +7,13 @@ the 8-GPU job), each run through the reference's own nmf_mu (oracle/_ref).  The 
 north_star, bit-exact iteration counts, labels (nmf.r:128 under both rules) and connectivity counts
 (nmf.r:140-143), and final H within 1e-9 relative Frobenius error.
 
-Three batches: the 28 first jobs on their own (small grids, both label rules through the engine's label
-kernel), and the two 1750-job shards the benches and the 8-GPU job run -- `bench.py --config C4` (125 restarts of
-every k: jobs 0..1749, which is also rank 0's shard) and rank 7's shard (jobs 12250..13999 of the whole
-1000-restart grid) -- with their real tile shapes, repacks and tail kernels.
+Round 5 added the first restart of every k inside each of shards 1..6 of the 8-GPU job (84 more reference jobs), so
+every shard holds reference jobs (test_golden_c4_covers_every_shard, CPU).
+
+Batches: the 28 first jobs on their own (small grids, both label rules through the engine's label kernel), and three
+1750-job shards as the benches and the 8-GPU job run them -- `bench.py --config C4` (125 restarts of every k: jobs
+0..1749, which is also rank 0's shard), rank 3's shard (jobs 5250..6999) and rank 7's shard (jobs 12250..13999 of the
+whole 1000-restart grid) -- with their real tile shapes, repacks and tail kernels.
 """
 import os
 
@@ -91,7 +94,7 @@ def test_c4_restarts_vs_reference(c4, c4_engine):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("shard", ["bench_rank0", "rank7"])
+@pytest.mark.parametrize("shard", ["bench_rank0", "rank3", "rank7"])
 def test_c4_gpu_shard_vs_reference(c4, c4_engine, shard):
     """A whole 1750-job per-GPU shard, as the bench / the 8-GPU job runs it: the golden jobs inside it bit-exact
     (iterations; argmax labels from the engine's label kernel, R-order labels as argmin of the engine's final H;
@@ -102,10 +105,10 @@ def test_c4_gpu_shard_vs_reference(c4, c4_engine, shard):
     nk, n = len(ks), int(g["c4_n"])
     if shard == "bench_rank0":     # bench.py --config C4 at N = 1: R = 1000 / 8 = 125 restarts of every k
         R, jb, je = 125, 0, 125 * nk
-    else:                          # rank 7 of the whole C4 job (R = 1000): distributed.shard_range(14000, 7, 8)
+    else:                          # rank 3 / 7 of the whole C4 job (R = 1000): distributed.shard_range(14000, r, 8)
         from nmfconsensus_amd.distributed import shard_range
         R = int(g["c4_R_total"])
-        jb, je = shard_range(nk * R, 7, 8)
+        jb, je = shard_range(nk * R, int(shard[4:]), 8)
     r = c4_engine.run(ks, R, maxiter=10000, seed=int(g["c4_seed"]), stop_rule=1, label_rule=0, job_begin=jb,
                       job_end=je, want_h=True)
     ids = g["c4_job_id"]

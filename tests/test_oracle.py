@@ -155,3 +155,25 @@ def test_reflib_generate_ran_is_errno_safe(golden):
     ref.L.generateMatrix(ctypes.byref(c(1000)), ctypes.byref(c(40)), ctypes.byref(c(3)), ctypes.byref(c(0)),
                          ctypes.byref(c(0)), ctypes.byref(c(1)), _d(W2), _d(H2), None, None)
     assert not W2.any() and not H2.any()
+
+
+def test_golden_c4_covers_every_shard():
+    """Every shard of the 8-GPU C4 job (distributed.shard_range(14000, r, 8)) holds reference jobs of every k in
+    tests/golden/golden_c4.npz (make_golden_c4.py), and the rank-3 shard's golden jobs carry their final H."""
+    import os
+
+    from nmfconsensus_amd.distributed import shard_range
+    path = os.path.join(os.path.dirname(__file__), "golden", "golden_c4.npz")
+    with np.load(path, allow_pickle=False) as z:
+        ids, ks, job_k = z["c4_job_id"], z["c4_ks"], z["c4_job_k"]
+        hjobs = np.concatenate([z[f"c4_Hjobs_k{int(k)}"] for k in ks])
+        R = int(z["c4_R_total"])
+    nk = len(ks)
+    assert np.array_equal(job_k, ks[ids % nk])
+    for r in range(8):
+        jb, je = shard_range(nk * R, r, 8)
+        inside = (ids >= jb) & (ids < je)
+        assert set(job_k[inside].tolist()) == set(ks.tolist()), r
+    jb, je = shard_range(nk * R, 3, 8)
+    pos3 = set(np.where((ids >= jb) & (ids < je))[0].tolist())
+    assert pos3 and pos3 <= set(hjobs.tolist())

@@ -241,6 +241,7 @@ float timeit(F f, int reps) {
 
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 200, reps = argc > 2 ? atoi(argv[2]) : 10;
+  const bool pmc = argc > 3 && !strcmp(argv[3], "pmc");   // counter passes: n = 500, one round, no checks / stamps
   const int m = 20000;
   // packing of R restarts of every k = 10..2 as the engine packs them (engine.hip pack()): k descending, first fit
   // into 16-column blocks (no restart across a block), four blocks to a 64-column panel
@@ -336,6 +337,7 @@ int main(int argc, char** argv) {
     printf("  %-44s %8.4f ms  %6.2f TF\n", name, ms, flop / ms / 1e9);
   };
   for (long n : {500L, 2000L}) {
+    if (pmc && n != 500) break;
     const long n_pad = (n + BK - 1) / BK * BK;
     const double flop = 2.0 * m * n * fk + 2.0 * m * fk2;   // one contraction (+ its k^2 part), every restart
     printf("\n== A h^T, n = %ld (n_pad %ld)\n", n, n_pad);
@@ -359,7 +361,7 @@ int main(int argc, char** argv) {
         {"  form BL+FD+E4", [&] { AF(F_BL | F_FD | F_E4); }},
         {"  form BL+FD+E4+EW", [&] { AF(F_BL | F_FD | F_E4 | F_EW); }},
     };
-    {   // every arm that keeps the arithmetic (V0 and the forms): one launch from the same W as one engine launch
+    if (!pmc) {   // every arm that keeps the arithmetic (V0 and the forms): one launch from the same W as one engine launch
       std::vector<double> x((size_t)cols * m_pad), y((size_t)cols * m_pad);
       for (auto& [name, launch] : arms) {
         if (name.find("V0") == std::string::npos && name.find("form") == std::string::npos) continue;
@@ -375,10 +377,11 @@ int main(int argc, char** argv) {
         printf("  %-44s output %s the engine's\n", name.c_str(), eq ? "bit-identical to" : "DIFFERS FROM");
       }
     }
-    {   // interleaved rounds (the chip's clock drifts with load and temperature): median and min per arm
-      for (int i = 0; i < 200; ++i) arms[0].second();   // ~1 s of load before the first round
+    auto interleaved = [&](std::vector<std::pair<std::string, std::function<void()>>>& arms) {
+      // interleaved rounds (the chip's clock drifts with load and temperature): median and min per arm
+      for (int i = 0; i < (pmc ? 2 : 200); ++i) arms[0].second();   // ~1 s of load before the first round
       CK(hipDeviceSynchronize());
-      const int rounds = 7;
+      const int rounds = pmc ? 1 : 7;
       std::vector<std::vector<float>> t(arms.size());
       for (int r = 0; r < rounds; ++r)
         for (size_t q = 0; q < arms.size(); ++q) t[q].push_back(timeit(arms[q].second, reps));
@@ -389,8 +392,9 @@ int main(int argc, char** argv) {
         printf("  %-44s %8.4f ms  %6.2f TF   (%6.2f)\n", arms[q].first.c_str(), v[v.size() / 2], flop / v[v.size() / 2] / 1e9,
                flop / v[0] / 1e9);
       }
-    }
-    {   // stamped probe: phase shares per wave and, per CU, how many of its workgroups are in their K loop
+    };
+    interleaved(arms);
+    if (!pmc) {   // stamped probe: phase shares per wave and, per CU, how many of its workgroups are in their K loop
       const long nw = (long)live * ngt * 4;
       AP(0, true);
       AP(0, true);
@@ -438,15 +442,22 @@ int main(int argc, char** argv) {
     const long n_cols_pad = (n + 127) / 128 * 128, g_ld = n_cols_pad, g_split = cols * g_ld;
     const int ntj = (int)(n_cols_pad / 128), ng = npanels / 4;
     printf("== W^T A, n = %ld (%d sample tiles)\n", n, ntj);
-#define WA(...) hipLaunchKernelGGL((k_wta2<__VA_ARGS__>), dim3(nsplit * ng * ntj), dim3(512), 0, 0, W, Ablk, m_pad, ng, ntj, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, (long)sq)
+#define WA(...) WAT(512, __VA_ARGS__)
+#define WAT(NTHR, ...) hipLaunchKernelGGL((k_wta2<__VA_ARGS__>), dim3(nsplit * ng * ntj), dim3(NTHR), 0, 0, W, Ablk, m_pad, ng, ntj, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, (long)sq)
+    std::vector<std::pair<std::string, std::function<void()>>> warms;
     if (ntj >= 4) {
-      report("k_wta2 big 4x128 nbuf3 (engine)", timeit([&] { WA(4, 128, 4, 2, 1, 3, 1, true); }, reps), flop);
-      report("  Gram from registers (GREG)", timeit([&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true); }, reps), flop);
-      report("  no Gram chains", timeit([&] { WA(4, 128, 4, 2, 1, 3, 1, true, false); }, reps), flop);
-      report("  nbuf 2", timeit([&] { WA(4, 128, 4, 2, 1, 2, 1, true); }, reps), flop);
+      warms = {
+          {"k_wta2 big 4x128 nbuf3 GREG (engine)", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true); }},
+          {"  Gram in LDS chains (round 3 form)", [&] { WA(4, 128, 4, 2, 1, 3, 1, true); }},
+          {"  no Gram chains", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, false); }},
+          {"  nbuf 2, LDS Gram", [&] { WA(4, 128, 4, 2, 1, 2, 1, true); }},
+          {"  16 waves (4 x 4), GREG", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); }},
+          {"  16 waves (4 x 4), no Gram", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, false); }},
+      };
     } else {
-      report("k_wta2 big 4x128 nbuf3 GPW2 (engine)", timeit([&] { WA(4, 128, 4, 2, 2, 3, 1, true); }, reps), flop);
+      warms = {{"k_wta2 big 4x128 nbuf3 GPW2 (engine)", [&] { WA(4, 128, 4, 2, 2, 3, 1, true); }}};
     }
+    interleaved(warms);
   }
   printf("done\n");
   return 0;
