@@ -50,9 +50,16 @@ typedef struct options_t {
  * runs on the GPU (HIP, gfx950).  Prints "Exiting nmf_mu after <iter>\n" like nmf_mu.c:296.
  * The stop rule is the reference's class-stability check (nmf_mu.c:253-282) in its defined
  * REF_COMPAT form.  Returns 0, or -1 on allocation / device failure (nmf_mu.c:138-151).
- * Ranks: 1 <= k <= min(m, n).  k = 2..16 runs on the MFMA engine (the team kernel for m <= 8192 genes, n <= 64
- * samples, else the batched engine with a batch of one); any other k on the generic GPU path (nmfc_mu_generic,
- * nmfconsensus_amd/csrc/generic.hip: plain fp64 products, one thread per output).  k outside 1..min(m, n) prints
+ * Ranks: 1 <= k <= min(m, n).  Routing, a function of (m, n, k) only (so a restart gives the same bits on every call):
+ *   solo    k = 2..4 on gct-sized matrices (nmfc_mu_solo_fits: m <= 1024, n <= 40): ONE workgroup runs the whole
+ *           restart, A resident in its register file (csrc/solo.hip, k_solo_mu);
+ *   team    other k = 2..16 with m_pad = 128-rounded m <= 8192, n <= 64: a team of m_pad / 64 workgroups
+ *           (k_team_mu, one launch with one upload / download);
+ *   engine  other k = 2..16: the batched MFMA engine with a batch of one;
+ *   generic any other k: plain fp64 products, one thread per output (nmfc_mu_generic, csrc/generic.hip).
+ * A team that cannot assemble (its workgroups not all resident, e.g. while other processes hold the GPU's CUs, as
+ * BatchJobs njobs > 1 runs it) reports so instead of waiting, and the restart runs on the engine; the solo kernel is
+ * one workgroup and needs no such fallback.  k outside 1..min(m, n) prints
  * "Error in nmf_mu: k=<k> unsupported (need 1 <= k <= min(m, n))" to stderr before any device work, leaves
  * w0/h0 untouched and returns -1.
  */

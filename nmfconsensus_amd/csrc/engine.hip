@@ -157,6 +157,10 @@ constexpr bool SMALL_NW8 = NMFC_SMALL_NW8 != 0;    // k_small_mu with eight wave
 #define NMFC_WTA_GREG 1
 #endif
 constexpr bool WTA_GREG = NMFC_WTA_GREG != 0;      // 4-panel W^T A tiles: diagonal Gram blocks from the tile's W registers
+#ifndef NMFC_WTA_W16
+#define NMFC_WTA_W16 1
+#endif
+constexpr bool WTA_W16 = NMFC_WTA_W16 != 0 && WTA_GREG;   // the 4-panel x 128-sample W^T A tile on 16 waves (4 per SIMD)
 constexpr int WTA_MID_NBUF = NMFC_WTA_MID_NBUF;    // ring depth of the 2-panel W^T A tile
 constexpr int WTA_MID_MINW = NMFC_WTA_MID_MINW;    // its launch-bounds waves per SIMD (4: two workgroups per CU)
 constexpr int AHTW_NBUF = NMFC_AHTW_NBUF;          // LDS ring depth of the full-width A h^T tiles
@@ -1065,10 +1069,14 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                  e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
-            auto kw = (ntj >= 4)   ? k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true, true, false, WTA_GREG>
+            // ntj >= 4: 16 waves (4 per SIMD, 64 x 32 outputs each; round 5: +2 % over 8 waves at full load, every
+            // Gram chain in registers, tools/kvar.hip), else 8 waves carrying 2 / 4 Gram candidates each
+            auto kw = (ntj >= 4)   ? (WTA_W16 ? k_wta2<WTA_NPT, 128, 4, 4, 1, GT_NBUF, 1, true, true, false, true>
+                                              : k_wta2<WTA_NPT, 128, 4, 2, 1, GT_NBUF, 1, true, true, false, WTA_GREG>)
                       : (ntj >= 2) ? k_wta2<WTA_NPT, 128, 4, 2, 2, GT_NBUF, 1, true>
                                    : k_wta2<WTA_NPT, 128, 4, 2, 4, GT_NBUF, 1, true>;
-            hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
+            const int wthr = (ntj >= 4 && WTA_W16) ? 1024 : 512;
+            hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(wthr), 0, st, e->W[cur].as<double>(),
                                e->Ablk.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
                                e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(),

@@ -46,6 +46,9 @@ __device__ __forceinline__ double mu_rule(double old, double num, double den) {
 // buffer load / store through it wrapped in a readfirstlane "waterfall" loop (round 5: 64 such loops around k_ahtw4's
 // W0 loads and W stores).
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+// The lane index by v_mbcnt: recomputed where it is used (two VALU instructions) instead of a value derived from
+// threadIdx.x before a K loop and held in a VGPR across it (the 16-wave W^T A tile has no register to spare).
+__device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // mu_rule without branches: the quotient and product are formed for every element and the zero cases selected after,
 // so a wave's rule is one straight instruction stream (no exec-mask branch per element).  The same bits as mu_rule for
@@ -102,11 +105,14 @@ __device__ __forceinline__ void step_barrier() {
 // QBLK: the Q operand is K-blocked ([K/16][rows][16] doubles: one 16-gene block of every row
 // contiguous, `ldq` = the total row count), so a stage of a tile is ONE contiguous RQ x 128 B run instead
 // of RQ rows 8 * ldq bytes apart.  The same canonical K order either way.
-// GREG: the wave may also accumulate one restart-diagonal 16 x 16 Gram block of its own P rows, block `gsel` of
-// its MB row blocks, into `gacc` -- W^T W from the W fragments already in registers for the tile MFMAs
-// (the A operand lane map (row fr, k g) and the B operand map (k g, col fr) hold the same value for P = Q),
-// in the canonical K order; gsel < 0: none.
-template <int RP, int RQ, int WR, int WC, int NBUF = GT_NBUF, bool QBLK = false, bool GREG = false>
+// GREG: the wave may also accumulate one 16 x 16 Gram block of its own P rows -- row block `gi` against row block
+// `gj` of its MB row blocks (gj = gi: a restart-diagonal block; gj = gi + 1: a block straddled by a restart) -- into
+// `gacc`: W^T W from the W fragments already in registers for the tile MFMAs (the A operand lane map (row fr, k g)
+// and the B operand map (k g, col fr) hold the same value for P = Q), in the canonical K order; gi < 0: none.
+// SPLIT (NBUF >= 3): the split-step form (below); false: each step computes its whole stage between the barriers
+// (one fragment set live instead of two: 24 VGPRs fewer at MB = 4, NB = 2, for the 16-wave tile).  Same order of
+// accumulation either way (kk = 0 then kk = 1 of every stage), so the same bits.
+template <int RP, int RQ, int WR, int WC, int NBUF = GT_NBUF, bool QBLK = false, bool GREG = false, bool SPLIT = true>
 struct GTile {
   static_assert(NBUF >= 2 && NBUF <= 16, "ring of 2..16 stages");
   static constexpr int NW = WR * WC;
@@ -123,7 +129,7 @@ struct GTile {
 
   d4 acc[MB][NB];
   d4 gacc;
-  int gsel = -1;   // GREG: wave-uniform
+  int gi = -1, gj = -1;   // GREG: wave-uniform
   __amdgpu_buffer_rsrc_t rp, rq;
   int voff[PPW];
   int qkm;
@@ -131,7 +137,7 @@ struct GTile {
 
   // P rows are K-contiguous at P + row*ldp, Q rows at Q + row*ldq (doubles); QBLK: Q + (k/16)*16*ldq + row*16
   __device__ __forceinline__ void bind(const double* P, long ldp, const double* Q, long ldq, int kend) {
-    const int w = (threadIdx.x >> 6) - wo, l = threadIdx.x & 63;
+    const int w = wave_id() - wo, l = threadIdx.x & 63;
     rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(P), 0, (int)(RP * ldp * 8), 0x00020000);
     rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Q), 0, QBLK ? (int)((long)kend * ldq * 8) : (int)(RQ * ldq * 8),
                                            0x00020000);
@@ -179,7 +185,7 @@ struct GTile {
     d2 a[MB], b[NB];
   };
   __device__ __forceinline__ void load_frag(const char* __restrict__ st, int kk, Frag& f) const {
-    const int w = (threadIdx.x >> 6) - wo, l = threadIdx.x & 63;
+    const int w = wave_id() - wo, l = threadIdx.x & 63;
     const int wr = w / WC, wc = w % WC;
     const int fr = l & 15, g = l >> 4;
     const char* sp = st + (wr * (RP / WR) + fr) * 128;
@@ -190,11 +196,16 @@ struct GTile {
 #pragma unroll
     for (int j = 0; j < NB; ++j) f.b[j] = *reinterpret_cast<const d2*>(sq + j * 16 * 128 + so);
   }
+  // GC: the wave's register Gram block.  GC_DYN: chosen at run time by gi (diagonal blocks only, a VGPR select of the
+  // fragment); -1: none; gi * 4 + gj: fixed at compile time (a K-loop instantiation per block: no selects, no branches)
+  static constexpr int GC_DYN = -2;
+  template <int GC = GC_DYN>
   __device__ __forceinline__ void mfma_frag(const Frag& f) {
     if constexpr (GT_PRIO) __builtin_amdgcn_s_setprio(1);
-    mfma_frag_body(f);
+    mfma_frag_body<GC>(f);
     if constexpr (GT_PRIO) __builtin_amdgcn_s_setprio(0);
   }
+  template <int GC = GC_DYN>
   __device__ __forceinline__ void mfma_frag_body(const Frag& f) {
 #pragma unroll
     for (int i = 0; i < MB; ++i)
@@ -204,12 +215,17 @@ struct GTile {
     for (int i = 0; i < MB; ++i)
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].y, f.b[j].y, acc[i][j], 0, 0, 0);
-    if constexpr (GREG) {
-      if (gsel >= 0) {
+    if constexpr (GREG && GC >= 0) {
+      constexpr int i = GC >> 2, j = GC & 3;
+      static_assert(i < MB && j < MB, "Gram block inside the wave's rows");
+      gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].x, f.a[j].x, gacc, 0, 0, 0);
+      gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i].y, f.a[j].y, gacc, 0, 0, 0);
+    } else if constexpr (GREG && GC == GC_DYN) {
+      if (gi >= 0) {
         d2 v = f.a[0];
 #pragma unroll
         for (int i = 1; i < MB; ++i)
-          if (gsel == i) v = f.a[i];
+          if (gi == i) v = f.a[i];
         gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, v.x, gacc, 0, 0, 0);
         gacc = __builtin_amdgcn_mfma_f64_16x16x4f64(v.y, v.y, gacc, 0, 0, 0);
       }
@@ -217,7 +233,7 @@ struct GTile {
   }
   template <int NKK = 2>
   __device__ __forceinline__ void compute(const char* __restrict__ st) {
-    const int w = (threadIdx.x >> 6) - wo, l = threadIdx.x & 63;
+    const int w = wave_id() - wo, l = threadIdx.x & 63;
     const int wr = w / WC, wc = w % WC;
     const int fr = l & 15, g = l >> 4;
     const char* sp = st + (wr * (RP / WR) + fr) * 128;
@@ -263,7 +279,7 @@ struct GTile {
   // and run returns false.  All waves must return the same answer.
   // LASTKK (NBUF == 2) = 1: the last stage's second half (K positions 8..15) holds zeros in both operands (the K
   // padding) and is skipped -- adding exact zeros to sums of non-negative products would change no bit.
-  template <int XL = 0, int LASTKK = 2, class Pre, class Extra, class AtLast>
+  template <int XL = 0, int LASTKK = 2, int GC = GC_DYN, class Pre, class Extra, class AtLast>
   __device__ __forceinline__ bool run(const double* __restrict__ P, long ldp, const double* __restrict__ Q, long ldq,
                                       int kbeg, int kend, char* __restrict__ smem, Pre pre, Extra extra, AtLast at_last) {
     static_assert(LASTKK == 2 || NBUF == 2, "half last stage on the two-stage ring only");
@@ -327,6 +343,32 @@ struct GTile {
     // kk = 0 (x, y) then kk = 1 (x, y) of every stage in order: the same sums bit for bit.
     // (the last step is peeled: no branch around the barrier, so the compiler's lgkmcnt for the kk = 1
     // fragments leaves the next stage's reads in flight)
+    if constexpr (!SPLIT) {
+      for (int s = 0; s < nst; ++s) {
+        const char* cur = smem + b * STAGE_BYTES;
+        if (s + D < nst) {
+          const int bd = (b + D >= NBUF) ? b + D - NBUF : b + D;
+          issue(base + bd * STAGE_BYTES, kbeg + (s + D) * BK2);
+          if (s + D + 1 == nst) {
+            at_last();
+            xl = true;
+          }
+        }
+        Frag f;
+        load_frag(cur, 0, f);
+        mfma_frag<GC>(f);
+        load_frag(cur, 1, f);
+        mfma_frag<GC>(f);
+        extra(cur);
+        if (s + 1 < nst) {
+          const int left = nst - s - 2;
+          wait_stages<D - 1, XL>(left < D - 1 ? left : D - 1, xl);
+          step_barrier();
+        }
+        b = (b + 1 == NBUF) ? 0 : b + 1;
+      }
+      return true;
+    }
     Frag f0, f1;
     load_frag(smem, 0, f0);
     for (int s = 0; s + 1 < nst; ++s) {
@@ -342,7 +384,7 @@ struct GTile {
         }
       }
       load_frag(cur, 1, f1);
-      mfma_frag(f0);
+      mfma_frag<GC>(f0);
       extra(cur);
       const int bn = (b + 1 == NBUF) ? 0 : b + 1;
       const int left = nst - s - 2;
@@ -351,15 +393,15 @@ struct GTile {
       step_barrier();   // also: every wave has read stage s (its kk = 1 fragments are in registers)
       load_frag(smem + bn * STAGE_BYTES, 0, f0);
       __builtin_amdgcn_sched_barrier(0);
-      mfma_frag(f1);
+      mfma_frag<GC>(f1);
       b = bn;
     }
     {   // last step (its DMA was issued D steps ago)
       const char* cur = smem + b * STAGE_BYTES;
       load_frag(cur, 1, f1);
-      mfma_frag(f0);
+      mfma_frag<GC>(f0);
       extra(cur);
-      mfma_frag(f1);
+      mfma_frag<GC>(f1);
     }
     return true;
   }
@@ -379,11 +421,11 @@ struct GTile {
 
   // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
   __device__ __forceinline__ static int row_of(int mb, int reg) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int w = wave_id(), l = lane_id();
     return (w / WC) * (RP / WR) + mb * 16 + (l >> 4) + 4 * reg;
   }
   __device__ __forceinline__ static int col_of(int nb) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int w = wave_id(), l = lane_id();
     return (w % WC) * (RQ / WC) + nb * 16 + (l & 15);
   }
 };
@@ -453,7 +495,7 @@ __device__ __forceinline__ void gram_cand(int cand, int& q, int& br, int& bc) {
 // of wave row wr, so at ntj = 4 the four chains of a workgroup sit on four SIMDs.  The straddling candidates (never
 // produced by the engine's 16-column block packing) keep the LDS form.  Same operands, same K order: bit-identical.
 template <int NPT, int RQ, int WR, int WC, int GPW, int NBUF = GT_NBUF, int MINW = 1, bool ABLK = false, bool GRAM = true,
-          bool GITEM = false, bool GREG = false>
+          bool GITEM = false, bool GREG = false, bool SPLIT = true>
 static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double* __restrict__ W, const double* __restrict__ Acm,
                                                               long m_pad, int ngroups, int ntj, int nsplit, int kchunk,
                                                               const int* __restrict__ prb, const int* __restrict__ pre,
@@ -462,7 +504,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
                                                               const int* __restrict__ stop_iter, double* __restrict__ Gpart,
                                                               long g_ld, long g_split, double* __restrict__ SWpart,
                                                               long sw_total) {
-  using T = GTile<64 * NPT, RQ, WR, WC, NBUF, ABLK, GREG>;
+  using T = GTile<64 * NPT, RQ, WR, WC, NBUF, ABLK, GREG, SPLIT>;
   static_assert(!GREG || (WR == NPT && GPW == 1 && GRAM && !GITEM), "register Gram: one panel per wave row");
   constexpr int NCAND = 7 * NPT;
   __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES + 64];
@@ -539,7 +581,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
   d4 gacc[GPW];
 #pragma unroll
   for (int x = 0; x < GPW; ++x) gacc[x] = (d4){0.0, 0.0, 0.0, 0.0};
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = wave_id(), l = threadIdx.x & 63;
   const int fr = l & 15, g = l >> 4;
   __syncthreads();   // need[] visible (no DMA in flight yet)
   int my_need[GPW], my_ra[GPW], my_rb[GPW];
@@ -553,7 +595,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
     if (cand < NCAND) {
       int q, br, bc;
       gram_cand<NPT>(cand, q, br, bc);
-      my_need[x] = (GREG && cand < 4 * NPT) ? 0 : need[cand];
+      my_need[x] = (GREG && (cand < 4 * NPT || WC == 4)) ? 0 : need[cand];
       my_ra[x] = 64 * q + 16 * br;
       my_rb[x] = 64 * q + 16 * bc;
       gram = GRAM && !GITEM && (gram || my_need[x]);
@@ -561,17 +603,32 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
   }
   if constexpr (GREG) {
     const int wr = w / WC, wc = w % WC;
-    int gs = -1;
-    if (wc == ((wr >> 1) & 1) % WC) {
+    int gi = -1, gj = -1;
+    if constexpr (WC == 4) {
+      // 16 waves: every Gram candidate of panel wr that falls to this workgroup (cand % ntj == t: at most two per
+      // panel for ntj >= 4) on its own wave of row wr, the k-th on wave column (t + wr + 2 k) & 3 -- the diagonal
+      // chains of a workgroup on four SIMDs (wave w runs on SIMD w & 3), a straddling one two SIMDs away
+      int kth = 0;
+#pragma unroll
+      for (int c = 0; c < 7; ++c) {   // panel wr's candidates: 4 diagonal blocks, then 3 straddling blocks
+        const int cand = c < 4 ? 4 * wr + c : 4 * NPT + 3 * wr + (c - 4);
+        if (cand % ntj != t) continue;
+        if (wc == ((t + wr + 2 * kth) & 3) && need[cand]) {
+          gi = c < 4 ? c : c - 4;
+          gj = c < 4 ? c : c - 3;
+        }
+        ++kth;
+      }
+    } else if (wc == ((wr >> 1) & 1) % WC) {   // WC = 2: the diagonal blocks, wave column (wr >> 1) & 1 of row wr
 #pragma unroll
       for (int br = 0; br < 4; ++br)
-        if ((4 * wr + br) % ntj == t && need[4 * wr + br]) gs = br;
+        if ((4 * wr + br) % ntj == t && need[4 * wr + br]) gi = gj = br;
     }
-    tl.gsel = __builtin_amdgcn_readfirstlane(gs);
+    tl.gi = __builtin_amdgcn_readfirstlane(gi);
+    tl.gj = __builtin_amdgcn_readfirstlane(gj);
   }
   const double* P = W + (long)pg * 64 * NPT * m_pad + kbeg;
-  tl.run(P, m_pad, Q, ldq, 0, kend - kbeg, smem, [&](const char* stg) {
-    if (!gram) return;
+  auto lds_gram = [&](const char* stg) {
 #pragma unroll
     for (int x = 0; x < GPW; ++x) {
       if (!my_need[x]) continue;
@@ -586,7 +643,32 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
         gacc[x] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b.y, gacc[x], 0, 0, 0);
       }
     }
-  });
+  };
+  // two instantiations of the K loop: the LDS Gram chains' accumulators are live only in the loop that runs them
+  // (a wave without an LDS chain -- every wave of a GREG tile under block packing -- keeps none of their registers)
+  constexpr bool LDSG = GRAM && !GITEM && !(GREG && WC == 4);   // the 16-wave GREG tile keeps every chain in registers
+  if constexpr (GREG && WC == 4) {
+    // one K-loop instantiation per register Gram block (4 diagonal, 3 straddling, none): the block is a compile-time
+    // constant in the MFMA stream, with no fragment select and no branch in the loop
+    auto go = [&](auto gc) {
+      tl.template run<0, 2, decltype(gc)::value>(P, m_pad, Q, ldq, 0, kend - kbeg, smem, [] { return true; },
+                                                 [](const char*) {}, [] {});
+    };
+    switch (tl.gi < 0 ? -1 : 4 * tl.gi + tl.gj) {
+      case 0: go(std::integral_constant<int, 0>{}); break;
+      case 5: go(std::integral_constant<int, 5>{}); break;
+      case 10: go(std::integral_constant<int, 10>{}); break;
+      case 15: go(std::integral_constant<int, 15>{}); break;
+      case 1: go(std::integral_constant<int, 1>{}); break;
+      case 6: go(std::integral_constant<int, 6>{}); break;
+      case 11: go(std::integral_constant<int, 11>{}); break;
+      default: go(std::integral_constant<int, -1>{}); break;
+    }
+  } else if (LDSG && gram) {
+    tl.run(P, m_pad, Q, ldq, 0, kend - kbeg, smem, lds_gram);
+  } else {
+    tl.run(P, m_pad, Q, ldq, 0, kend - kbeg, smem, [](const char*) {});
+  }
   double* out = Gpart + (long)s * g_split + (long)pg * 64 * NPT * g_ld + (long)t * RQ;
 #pragma unroll
   for (int mb = 0; mb < T::MB; ++mb)
@@ -599,10 +681,11 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
     double* so = SWpart + (long)s * sw_total;
     const int pnl = ra >> 6;
     const ColInfo* cp = ci + (long)(NPT * pg + pnl) * PANEL;
+    const int ln = lane_id();   // not the pre-loop lane values: nothing lane-derived held across the K loop
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
-      const int lr = (ra & 63) + g + 4 * reg;
-      const int lcn = (rb & 63) + fr;
+      const int lr = (ra & 63) + (ln >> 4) + 4 * reg;
+      const int lcn = (rb & 63) + (ln & 15);
       const ColInfo cr = cp[lr];
       if (cr.k == 0 || cr.lc0 != cp[lcn].lc0 || cp[lcn].k == 0) continue;
       const int a = lr - cr.lc0, b = lcn - cr.lc0;
@@ -616,10 +699,7 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
       if (my_need[x]) put_gram(my_ra[x], my_rb[x], gacc[x]);
   }
   if constexpr (GREG) {
-    if (tl.gsel >= 0) {
-      const int rr = 64 * (w / WC) + 16 * tl.gsel;
-      put_gram(rr, rr, tl.gacc);
-    }
+    if (tl.gi >= 0) put_gram(64 * (w / WC) + 16 * tl.gi, 64 * (w / WC) + 16 * tl.gj, tl.gacc);
   }
 }
 

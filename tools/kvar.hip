@@ -444,6 +444,71 @@ int main(int argc, char** argv) {
     printf("== W^T A, n = %ld (%d sample tiles)\n", n, ntj);
 #define WA(...) WAT(512, __VA_ARGS__)
 #define WAT(NTHR, ...) hipLaunchKernelGGL((k_wta2<__VA_ARGS__>), dim3(nsplit * ng * ntj), dim3(NTHR), 0, 0, W, Ablk, m_pad, ng, ntj, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, (long)sq)
+    if (!pmc && ntj >= 4) {   // the 16-wave tile's G and Gram partials against the engine's 8-wave tile, bit for bit
+      const size_t gn = (size_t)nsplit * g_split, sn = (size_t)nsplit * sq;
+      std::vector<double> g1(gn), g2(gn), s1(sn), s2(sn);
+      auto grab = [&](std::vector<double>& g, std::vector<double>& sw, auto launch) {
+        CK(hipMemset(Gpart, 0xff, sizeof(double) * gn));
+        CK(hipMemset(SWpart, 0xff, sizeof(double) * sn));
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(g.data(), Gpart, sizeof(double) * gn, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(sw.data(), SWpart, sizeof(double) * sn, hipMemcpyDeviceToHost));
+      };
+      grab(g1, s1, [&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true); });
+      grab(g2, s2, [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); });
+      printf("  16-wave GREG vs engine (block packing): G partials %s, Gram partials %s\n",
+             memcmp(g1.data(), g2.data(), sizeof(double) * gn) ? "DIFFER" : "bit-identical",
+             memcmp(s1.data(), s2.data(), sizeof(double) * sn) ? "DIFFER" : "bit-identical");
+      // contiguous packing (restarts straddle 16-column blocks, never panels): every straddling Gram block through
+      // the 16-wave tile's register chains against the 8-wave tile's LDS chains
+      std::vector<ColInfo> cj((size_t)npanels * PANEL, ColInfo{0, 0, 0, 0});
+      std::vector<RestartInfo> rj;
+      std::vector<int> pb(npanels, 0), pe(npanels, 0);
+      int col = 0, sqj = 0, nstr = 0;
+      for (int k = 10; k >= 2; --k)
+        for (int r = 0; r < R; ++r) {
+          if (col % PANEL + k > PANEL) col = (col / PANEL + 1) * PANEL;
+          if (col + k > npanels * PANEL) break;
+          const int id = (int)rj.size();
+          rj.push_back({col, k, id, sqj});
+          for (int a = 0; a < k; ++a) cj[(size_t)col + a] = ColInfo{sqj, col % PANEL, k, id};
+          nstr += (col >> 4) != ((col + k - 1) >> 4);
+          sqj += k * k;
+          col += k;
+        }
+      for (int p = 0; p < npanels; ++p) {
+        pb[p] = (int)rj.size();
+        pe[p] = (int)rj.size();
+      }
+      for (size_t q = rj.size(); q-- > 0;) pb[rj[q].col0 / PANEL] = (int)q;
+      for (size_t q = 0; q < rj.size(); ++q) pe[rj[q].col0 / PANEL] = (int)q + 1;
+      for (int p = 0; p < npanels; ++p)
+        if (pe[p] < pb[p]) pe[p] = pb[p];
+      std::vector<ColInfo> ci_save(cols);
+      CK(hipMemcpy(ci_save.data(), dci, sizeof(ColInfo) * cols, hipMemcpyDeviceToHost));
+      std::vector<RestartInfo> ri_save(nall);
+      CK(hipMemcpy(ri_save.data(), dri, sizeof(RestartInfo) * nall, hipMemcpyDeviceToHost));
+      std::vector<int> pbs(npanels), pes(npanels);
+      CK(hipMemcpy(pbs.data(), dprb, sizeof(int) * npanels, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(pes.data(), dpre, sizeof(int) * npanels, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(dci, cj.data(), sizeof(ColInfo) * cols, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dri, rj.data(), sizeof(RestartInfo) * std::min<size_t>(rj.size(), nall), hipMemcpyHostToDevice));
+      CK(hipMemcpy(dprb, pb.data(), sizeof(int) * npanels, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dpre, pe.data(), sizeof(int) * npanels, hipMemcpyHostToDevice));
+      const size_t sj = std::min<size_t>((size_t)sqj, (size_t)sq);
+      grab(g1, s1, [&] { WA(4, 128, 4, 2, 1, 3, 1, true); });
+      grab(g2, s2, [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); });
+      bool same_sw = true;
+      for (int sp = 0; sp < nsplit; ++sp)
+        same_sw = same_sw && !memcmp(s1.data() + (size_t)sp * sq, s2.data() + (size_t)sp * sq, sizeof(double) * sj);
+      printf("  16-wave GREG vs 8-wave LDS Gram (contiguous packing, %d of %zu restarts straddle a block): Gram partials %s\n",
+             nstr, rj.size(), same_sw ? "bit-identical" : "DIFFER");
+      CK(hipMemcpy(dci, ci_save.data(), sizeof(ColInfo) * cols, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dri, ri_save.data(), sizeof(RestartInfo) * nall, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dprb, pbs.data(), sizeof(int) * npanels, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dpre, pes.data(), sizeof(int) * npanels, hipMemcpyHostToDevice));
+    }
     std::vector<std::pair<std::string, std::function<void()>>> warms;
     if (ntj >= 4) {
       warms = {
@@ -451,8 +516,11 @@ int main(int argc, char** argv) {
           {"  Gram in LDS chains (round 3 form)", [&] { WA(4, 128, 4, 2, 1, 3, 1, true); }},
           {"  no Gram chains", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, false); }},
           {"  nbuf 2, LDS Gram", [&] { WA(4, 128, 4, 2, 1, 2, 1, true); }},
-          {"  16 waves (4 x 4), GREG", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); }},
           {"  16 waves (4 x 4), no Gram", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, false); }},
+          {"  16 waves, GREG", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); }},
+          {"  16 waves, GREG, unsplit steps", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true, false); }},
+          {"  16 waves, LDS Gram, unsplit steps", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, false, false); }},
+          {"  8 waves, GREG, unsplit steps", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true, false); }},
       };
     } else {
       warms = {{"k_wta2 big 4x128 nbuf3 GPW2 (engine)", [&] { WA(4, 128, 4, 2, 2, 3, 1, true); }}};

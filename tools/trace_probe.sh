@@ -10,5 +10,5 @@ for R in ${RS:-25 200}; do
     python3 bench.py --restarts "$R" --steps 1 --warmup 0 --no-cpu-baseline --dump-iters "$OUT/R$R.iters.npy" ${BENCH_ARGS:-} > "$OUT/R$R.log" 2>&1 \
     || { echo "trace R=$R failed"; tail -5 "$OUT/R$R.log"; exit 1; }
   f=$(find "$OUT/R$R" -name '*kernel_trace.csv' | head -1)
-  python3 tools/trace_timeline.py "$f" 100 "$OUT/R$R.iters.npy" > "$OUT/R$R.timeline.txt" && echo "R=$R" && cat "$OUT/R$R.timeline.txt"
+  python3 tools/trace_timeline.py "$f" ${BUCKET:-100} "$OUT/R$R.iters.npy" > "$OUT/R$R.timeline.txt" && echo "R=$R" && cat "$OUT/R$R.timeline.txt"
 done
