@@ -149,6 +149,10 @@ constexpr int NARROW_NBUF = NMFC_NARROW_NBUF;      // LDS ring depth of the narr
 #ifndef NMFC_WTA_MID_MINW
 #define NMFC_WTA_MID_MINW 1
 #endif
+#ifndef NMFC_WTA_MID_GREG
+#define NMFC_WTA_MID_GREG 1
+#endif
+constexpr bool WTA_MID_GREG = NMFC_WTA_MID_GREG != 0;   // 2-panel W^T A tile: 2 x 4 waves, Gram chains in registers
 #ifndef NMFC_SMALL_NW8
 #define NMFC_SMALL_NW8 1
 #endif
@@ -1083,8 +1087,11 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                sw_total);
           } else if (wta_mid) {   // npanels is a multiple of WTA_NPT, so of 2
             const int ng = (lp + 1) / 2;
-            auto kw = (ntj >= 2) ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW, true>
-                                 : k_wta2<2, 128, 4, 2, 2, WTA_MID_NBUF, WTA_MID_MINW, true>;
+            // ntj >= 4: wave rows = panels (2 x 4 waves, 64 x 32 outputs each) with every Gram chain in registers
+            // (the 16-wave big tile's scheme), else 4 x 2 waves carrying LDS Gram chains
+            auto kw = (ntj >= 4 && WTA_MID_GREG) ? k_wta2<2, 128, 2, 4, 1, WTA_MID_NBUF, WTA_MID_MINW, true, true, false, true>
+                      : (ntj >= 2)               ? k_wta2<2, 128, 4, 2, 1, WTA_MID_NBUF, WTA_MID_MINW, true>
+                                                 : k_wta2<2, 128, 4, 2, 2, WTA_MID_NBUF, WTA_MID_MINW, true>;
             hipLaunchKernelGGL(kw, dim3(e->nsplit * ng * ntj), dim3(512), 0, st, e->W[cur].as<double>(),
                                e->Ablk.as<double>(), e->m_pad, ng, ntj, e->nsplit, e->kchunk, e->prb.as<int>(),
                                e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
