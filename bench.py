@@ -342,6 +342,7 @@ def main():
         ach = kernels[dom]["tflops"]
         roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                "frac_metric": "algorithmic fp64 TFLOP/s (2mnk + 2mk^2 per live restart) / 78.6 TF", "frac_metric_version": 1,
                 "algo_bytes_per_launch": kernels[dom]["algo_bytes_per_launch"], "kernels": kernels,
                 "note": ("achieved = algorithmic flop per launch (SURVEY 8(d): 2mnk + 2mk^2 per live restart) / "
                          "the kernel's mean HIP-event duration over the timed launches of the timed sweeps (every "
@@ -452,6 +453,7 @@ def bench_c1(args, dev):
         ach = fl / (ms / c * 1e-3) / 1e12
         roof = {"bound": "mfma", "kernel": "small_mu", "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                "frac_metric": "algorithmic fp64 TFLOP/s / 78.6 TF", "frac_metric_version": 1,
                 "note": "one persistent launch runs the whole sweep's MU loops (k_small_mu): algorithmic flop of all "
                         "restart-iterations (4mnk + 4(m+n)k^2 each) / its HIP-event duration; latency-bound (the "
                         "longest 16-column block sets the launch), SURVEY 8(d): C1/C2 fit in L2"}
@@ -779,6 +781,10 @@ def bench_brunet(args, rank, world, local, dev):
         sweep_ops = float(np.sum(m * n * np.array([brunet_valu_ops_per_element(int(k)) for k in ks_job]) * res.iters)) * world
         roof = {"bound": "valu", "kernel": dom, "achieved": ach, "peak": FP64_VALU_PEAK_TOPS,
                 "unit": "T fp64 VALU lane-instructions/s", "frac": ach / FP64_VALU_PEAK_TOPS, "traffic": None,
+                # what `frac` measures (round 4 changed it from rank-k TFLOP/s vs 78.6 TF, which stays as
+                # rank_k_frac_of_78.6TF): compare lines of the same frac_metric only
+                "frac_metric": "fp64 VALU lane-instructions / 39.3 T (2k + BRUNET_DIV_OPS per quotient, pinned to "
+                               "the ISA by tests/test_kernel_resources.py)", "frac_metric_version": 2,
                 "kernels": kernels,
                 "rank_k_tflops": kernels[dom]["tflops"], "rank_k_frac_of_78.6TF": kernels[dom]["tflops"] / FP64_MFMA_PEAK_TFLOPS,
                 "sweep_valu_tops": sweep_ops / (elapsed / args.steps) / 1e12,

@@ -87,6 +87,9 @@ void nmfc_engine_destroy(nmfc_engine* e);
 /* The HIP device ordinal the engine was created on (resolved at creation when device was -1); -1 for NULL. */
 int nmfc_engine_device(const nmfc_engine* e);
 
+/* The calling thread's current HIP device ordinal (what device -1 resolves to), or -1 on failure. */
+int nmfc_current_device(void);
+
 void nmfc_default_opts(nmfc_sweep_opts* o);
 
 /* Runs the k-sweep: for every job of the shard, init (generateMatrix(ran) stream with the job seed,

@@ -56,7 +56,7 @@ EXPORTED = [
     "nmf_mu", "set_default_opts", "checkArguments", "checkMatrices", "randnumber", "generateMatrix",
     "calculateNorm", "calculateMaxchange",
     # include/nmfc.h
-    "nmfc_engine_create", "nmfc_engine_destroy", "nmfc_engine_device", "nmfc_engine_mu1", "nmfc_mu_generic", "nmfc_mu_solo_fits", "nmfc_mu_solo", "nmfc_brunet_device", "nmfc_default_opts", "nmfc_engine_run", "nmfc_sweep",
+    "nmfc_engine_create", "nmfc_engine_destroy", "nmfc_engine_device", "nmfc_current_device", "nmfc_engine_mu1", "nmfc_mu_generic", "nmfc_mu_solo_fits", "nmfc_mu_solo", "nmfc_brunet_device", "nmfc_default_opts", "nmfc_engine_run", "nmfc_sweep",
     "nmfc_consensus", "nmfc_cophenetic", "nmfc_cophenetic_batch", "nmfc_cutree", "nmfc_last_error", "nmfc_version", "nmfc_engine_kernel_time",
     "nmfc_engine_set_timing", "nmfc_engine_kernel_flops", "nmfc_engine_kernel_bytes",
     "nmfc_calculate_norm_dev", "nmfc_calculate_maxchange_dev", "nmfc_nmf_mu_release",
@@ -105,6 +105,8 @@ def lib() -> ctypes.CDLL:
     L.nmfc_engine_destroy.restype = None
     L.nmfc_engine_device.argtypes = [ctypes.c_void_p]
     L.nmfc_engine_device.restype = c_int
+    L.nmfc_current_device.argtypes = []
+    L.nmfc_current_device.restype = c_int
     L.nmfc_engine_mu1.argtypes = [ctypes.c_void_p, c_int, c_int, c_int, _dp, _dp, _dp, _dp, ip, ip]
     L.nmfc_engine_mu1.restype = c_int
     L.nmfc_mu_generic.argtypes = [_dp, c_int, c_int, c_int, c_int, c_int, _dp, _dp, ip, ip]

@@ -716,6 +716,11 @@ void nmfc_engine_destroy(nmfc_engine* e) {
 
 int nmfc_engine_device(const nmfc_engine* e) { return e ? e->dev : -1; }
 
+int nmfc_current_device(void) {
+  int d = -1;
+  return hipGetDevice(&d) == hipSuccess ? d : -1;
+}
+
 void nmfc_engine_set_timing(nmfc_engine* e, int enable) {
   if (!e) return;
   e->timing = enable > 0;
@@ -995,6 +1000,9 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         // at most the CUs k_small_mu leaves free (one workgroup of either kernel fills a CU), shared by the solo
         // launches in proportion to their jobs: the block kernel's workgroups -- the sweep's critical path on C2 --
         // never wait for a CU behind solo workgroups; a solo workgroup runs its share of jobs one after another
+        // (the budget assumes this engine is the only one on the device: restart groups -- several engines on one
+        // GPU, distributed.RestartGroups -- are a large-shape tool and would oversubscribe it here; a speed matter
+        // only, the bits do not depend on it)
         const long free_cu = team ? e->ncu : std::max<long>(1, e->ncu - (long)sblocks.size());
         size_t g0 = 0;
         for (int q = 0; g0 < solo.size(); ++q) {

@@ -240,13 +240,19 @@ _DONMF_LOCK = threading.Lock()
 
 def _donmf_engine(A: np.ndarray, device: int) -> "Engine":
     """The Engine doNMF reuses across calls (nmf.r calls doNMF once per restart on one matrix): kept while A is
-    byte-identical to the cached host copy and the device is the same; anything else builds a new one."""
+    byte-identical to the cached host copy and the device is the same; anything else builds a new one.  device -1
+    is resolved to the calling thread's current HIP device first, so a change of current device between calls
+    builds a new engine instead of reusing the one on the old device."""
+    from . import _lib
+
+    if device < 0:
+        device = _lib.lib().nmfc_current_device()
     c = _DONMF
     if c["eng"] is not None and c["device"] == device and c["A"].shape == A.shape and np.array_equal(c["A"], A):
         return c["eng"]
     release_doNMF_engine_locked()
     c["eng"] = Engine(A, device)
-    c["A"], c["device"] = A.copy(order="F"), device
+    c["A"], c["device"] = A.copy(order="F"), c["eng"].device
     return c["eng"]
 
 
