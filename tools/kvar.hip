@@ -211,6 +211,49 @@ static __global__ __launch_bounds__(256, 3) void k_ahtw_probe(int iter, const do
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// FETCH_SIZE calibration (kvar cal): read a known number of bytes with the access patterns of the engine's MFMA kernels
+// and compare with the counter (MI355X_MICROARCH.md: FETCH_SIZE under-counts wide coalesced streams up to 2x; the
+// factor depends on the pattern).  k_cal_b64: the A h^T epilogue's W0 loads (buffer_load_b64, each instruction 4 rows
+// x 128 B) over W; k_cal_dma: the GTile operand stream (buffer_load ... lds, 1 KiB per wave instruction) over W.
+// ---------------------------------------------------------------------------------------------------------------
+static __global__ __launch_bounds__(256) void k_cal_b64(const double* __restrict__ W, long m_pad, int npanels, int ngt,
+                                                        double* __restrict__ out) {
+  const int b = blockIdx.x, p = b / ngt, gt = b % ngt, w = wave_id(), lane = threadIdx.x & 63;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(W) + (long)p * PANEL * m_pad + (long)gt * GT + (GT / 4) * w, 0, (int)(PANEL * m_pad * 8), 0x00020000);
+  const int wvoff = (int)(((lane >> 4) * m_pad + (lane & 15)) * 8);
+  double acc = 0.0;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+        acc += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                              rw, wvoff, (int)(((16 * mb + 4 * reg) * m_pad + 16 * nb) * 8), 0));
+  out[(long)b * 256 + threadIdx.x] = acc;
+}
+
+static __global__ __launch_bounds__(256) void k_cal_dma(const double* __restrict__ W, long m_pad, long cols,
+                                                        double* __restrict__ out) {
+  // workgroup b streams rows [64 b, 64 b + 64) of W (m_pad doubles each) through LDS in 1 KiB pieces
+  __shared__ __attribute__((aligned(1024))) char lds[4096];
+  const int w = wave_id(), lane = threadIdx.x & 63;
+  const long row0 = (long)blockIdx.x * 64;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(W) + row0 * m_pad, 0,
+                                                                     (int)(64 * m_pad * 8), 0x00020000);
+  const long bytes = 64 * m_pad * 8;
+  for (long off = (long)w * 1024; off < bytes; off += 4 * 1024) {
+    lds_dma16(r, (uint32_t)(uintptr_t)lds + w * 1024, lane * 16, (int)off);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  out[(long)blockIdx.x * 256 + threadIdx.x] = reinterpret_cast<const double*>(lds)[threadIdx.x & 127];
+  (void)cols;
+}
+
 #define CK(x)                                                                                 \
   do {                                                                                        \
     hipError_t e_ = (x);                                                                      \
@@ -242,6 +285,7 @@ float timeit(F f, int reps) {
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 200, reps = argc > 2 ? atoi(argv[2]) : 10;
   const bool pmc = argc > 3 && !strcmp(argv[3], "pmc");   // counter passes: n = 500, one round, no checks / stamps
+  const bool cal = argc > 3 && !strcmp(argv[3], "cal");   // FETCH_SIZE calibration kernels only
   const int m = 20000;
   // packing of R restarts of every k = 10..2 as the engine packs them (engine.hip pack()): k descending, first fit
   // into 16-column blocks (no restart across a block), four blocks to a 64-column panel
@@ -336,6 +380,18 @@ int main(int argc, char** argv) {
   auto report = [&](const char* name, float ms, double flop) {
     printf("  %-44s %8.4f ms  %6.2f TF\n", name, ms, flop / ms / 1e9);
   };
+  if (cal) {   // each calibration kernel twice; the known bytes are printed for tools/pmc_cal.py
+    double* o;
+    CK(hipMalloc(&o, sizeof(double) * 256 * (size_t)live * ngt));
+    for (int r = 0; r < 2; ++r) {
+      hipLaunchKernelGGL(k_cal_b64, dim3(live * ngt), dim3(256), 0, 0, W, m_pad, live, ngt, o);
+      hipLaunchKernelGGL(k_cal_dma, dim3(live), dim3(256), 0, 0, W, m_pad, cols, o);
+    }
+    CK(hipDeviceSynchronize());
+    printf("cal k_cal_b64 bytes %.0f\ncal k_cal_dma bytes %.0f\n", (double)live * PANEL * m_pad * 8,
+           (double)live * PANEL * m_pad * 8);
+    return 0;
+  }
   for (long n : {500L, 2000L}) {
     if (pmc && n != 500) break;
     const long n_pad = (n + BK - 1) / BK * BK;
