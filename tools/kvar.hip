@@ -574,6 +574,11 @@ int main(int argc, char** argv) {
           {"  nbuf 2, LDS Gram", [&] { WA(4, 128, 4, 2, 1, 2, 1, true); }},
           {"  16 waves (4 x 4), no Gram", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, false); }},
           {"  16 waves, GREG", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); }},
+          {"  16 waves, GREG, first 6 x 256 items only", [&] {
+             hipLaunchKernelGGL((k_wta2<4, 128, 4, 4, 1, 3, 1, true, true, false, true>), dim3(std::min(6 * 256, nsplit * ng * ntj)),
+                                dim3(1024), 0, 0, W, Ablk, m_pad, ng, ntj, nsplit, kchunk, dprb, dpre, dri, dci, stop, Gpart,
+                                g_ld, g_split, SWpart, (long)sq);
+           }},
           {"  16 waves, GREG, unsplit steps", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true, false); }},
           {"  16 waves, LDS Gram, unsplit steps", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, false, false); }},
           {"  8 waves, GREG, unsplit steps", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true, false); }},
