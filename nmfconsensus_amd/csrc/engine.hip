@@ -272,9 +272,10 @@ int live_panels(const Packing& pk) {
   return np;
 }
 
-// Small-shape path, restarts that the one-workgroup solo kernel takes (nmfc_mu_solo_fits(m, n, k): rank <= 4 on
-// gct-sized shapes): each gets 4 stacked columns of its own after the k_small_mu blocks (cols from col_base), in
-// order of kernel rank (one launch per rank), then restart id.  Returns the solo jobs; pk grows to hold them.
+// Small-shape path, restarts that the one-workgroup solo kernels take (nmfc_mu_solo_fits(m, n, k): rank <= 8 on
+// gct-sized shapes): each gets 4 (kernel rank <= 4) or 8 stacked columns of its own after the k_small_mu blocks
+// (cols from col_base), in order of kernel rank (one launch per rank), then restart id.  Returns the solo jobs; pk
+// grows to hold them.
 std::vector<SoloJob> place_solo(Packing& pk, std::vector<RestartInfo> solo, int col_base, int n) {
   std::stable_sort(solo.begin(), solo.end(), [n](const RestartInfo& a, const RestartInfo& b) {
     const int ka = nmfc_solo_batch_rank(n, a.k), kb = nmfc_solo_batch_rank(n, b.k);
@@ -284,7 +285,7 @@ std::vector<SoloJob> place_solo(Packing& pk, std::vector<RestartInfo> solo, int 
   int col = col_base;
   for (RestartInfo r : solo) {
     r.col0 = col;
-    col += 4;
+    col += nmfc_solo_batch_rank(n, r.k) <= 4 ? 4 : 8;
     pk.ri.push_back(r);
     jobs.push_back(SoloJob{r.col0, r.k, r.rid, 0});
   }
@@ -328,8 +329,8 @@ struct nmfc_engine {
   bool narrow_lc = true;            // env NMFC_NARROW_LC=0: the one-wave narrow W^T A kernel
   bool gram_model = true;           // env NMFC_GRAM_MODEL=0: the tile cost model without the Gram workgroups
   bool solo_ok = true;              // env NMFC_SOLO=0: no solo kernel (every small-shape restart in k_small_mu blocks)
-  hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // the solo launches (one per kernel rank) beside k_small_mu
-  hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
+  hipStream_t aux[4] = {nullptr, nullptr, nullptr, nullptr};   // the solo launches (one per kernel rank: 2, 3, 4, 8)
+  hipEvent_t fork_ev = nullptr, join_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   int team_occ = 0;                // resident k_team_mu workgroups per CU (occupancy query, once)
   // nmfc_engine_mu1 (one restart, the nmf_mu drop-in): device and pinned staging [block | stop | W | H],
   // its own partial buffers and flags (zeroed when allocated; tags continue from mu1_base, the iterations of
@@ -703,7 +704,7 @@ void nmfc_engine_destroy(nmfc_engine* e) {
                     &e->teamFlag,  &e->mu1_dev,   &e->mu1_G,     &e->mu1_SW,    &e->mu1_flag};
   for (DevBuf* b : bufs) b->release();
   e->solojobs.release();
-  for (int q = 0; q < 3; ++q) {
+  for (int q = 0; q < 4; ++q) {
     if (e->aux[q]) (void)hipStreamDestroy(e->aux[q]);
     if (e->join_ev[q]) (void)hipEventDestroy(e->join_ev[q]);
   }
@@ -981,7 +982,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     if (!solo.empty()) {
       if (e->solojobs.ensure(sizeof(SoloJob) * solo.size())) return -1;
       HCHECK(hipMemcpyAsync(e->solojobs.p, solo.data(), sizeof(SoloJob) * solo.size(), hipMemcpyHostToDevice, st));
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < 4; ++q) {
         if (!e->aux[q]) HCHECK(hipStreamCreateWithFlags(&e->aux[q], hipStreamNonBlocking));
         if (!e->join_ev[q]) HCHECK(hipEventCreateWithFlags(&e->join_ev[q], hipEventDisableTiming));
       }
@@ -996,31 +997,45 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       if (!sblocks.empty() && launch_small(e, (int)sblocks.size(), opts.maxiter, opts.stop_rule)) return -1;
       if (!solo.empty()) {
         // beside k_small_mu on streams of their own (one launch per kernel rank), after it when teams run (a team's
-        // workgroups must all be resident at once: nothing else may hold CUs then)
-        // at most the CUs k_small_mu leaves free (one workgroup of either kernel fills a CU), shared by the solo
-        // launches in proportion to their jobs: the block kernel's workgroups -- the sweep's critical path on C2 --
-        // never wait for a CU behind solo workgroups; a solo workgroup runs its share of jobs one after another
+        // workgroups must all be resident at once: nothing else may hold CUs then).
+        // Beside the block kernel: at most the CUs k_small_mu leaves free (one workgroup of either kernel fills a
+        // CU), shared by the solo launches in proportion to their jobs weighted by the kernels' cost per iteration
+        // (tools/solo_iter_time.py: rank 2 ~3.7 us, 3..4 ~5.7, 5..8 ~12.2), so the block kernel's workgroups never
+        // wait for a CU behind solo workgroups, and each solo workgroup runs its share of jobs one after another
         // (the budget assumes this engine is the only one on the device: restart groups -- several engines on one
         // GPU, distributed.RestartGroups -- are a large-shape tool and would oversubscribe it here; a speed matter
-        // only, the bits do not depend on it)
+        // only, the bits do not depend on it).  Without blocks (every job a solo job): one workgroup per job, the
+        // launches issued from the highest kernel rank down, so the dispatcher starts the costliest jobs first and
+        // fills the CUs that free up with the rest, across the launches.
+        const bool alone = sblocks.empty() || team;
         const long free_cu = team ? e->ncu : std::max<long>(1, e->ncu - (long)sblocks.size());
-        size_t g0 = 0;
-        for (int q = 0; g0 < solo.size(); ++q) {
+        auto wt = [](int kp) -> long { return kp <= 2 ? 4 : kp <= 4 ? 6 : 12; };
+        long wsum = 0;
+        for (const SoloJob& jb : solo) wsum += wt(nmfc_solo_batch_rank(n, jb.k));
+        std::vector<std::pair<size_t, size_t>> groups;   // [g0, g1) of one kernel rank, ascending
+        for (size_t g0 = 0; g0 < solo.size();) {
           const int kp = nmfc_solo_batch_rank(n, solo[g0].k);
           size_t g1 = g0;
           while (g1 < solo.size() && nmfc_solo_batch_rank(n, solo[g1].k) == kp) ++g1;
+          groups.emplace_back(g0, g1);
+          g0 = g1;
+        }
+        for (int q = 0; q < (int)groups.size(); ++q) {
+          const size_t g0 = groups[groups.size() - 1 - q].first, g1 = groups[groups.size() - 1 - q].second;
+          const int kp = nmfc_solo_batch_rank(n, solo[g0].k);
+          const long nq = (long)(g1 - g0);
+          const long share = alone ? nq : std::min<long>(nq, std::max<long>(1, free_cu * nq * wt(kp) / wsum));
           hipStream_t sq = team ? st : e->aux[q];
           if (!team) HCHECK(hipStreamWaitEvent(sq, e->fork_ev, 0));
           if (nmfc_solo_batch_launch(e->Acm.as<double>(), e->m_pad, m, n, e->W[0].as<double>(), e->m_pad,
-                                     e->H[0].as<double>(), e->n_pad, e->solojobs.as<SoloJob>() + g0, (int)(g1 - g0), kp,
+                                     e->H[0].as<double>(), e->n_pad, e->solojobs.as<SoloJob>() + g0, (int)nq, kp,
                                      opts.maxiter, opts.stop_rule, e->stop_iter.as<int>(), e->stop_reason.as<int>(),
-                                     (int)std::max<long>(1, free_cu * (long)(g1 - g0) / (long)solo.size()), sq))
+                                     (int)share, sq))
             return -1;
           if (!team) {
             HCHECK(hipEventRecord(e->join_ev[q], sq));
             HCHECK(hipStreamWaitEvent(st, e->join_ev[q], 0));
           }
-          g0 = g1;
         }
       }
     }

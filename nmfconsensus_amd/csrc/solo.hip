@@ -395,6 +395,368 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
   }   // jobs
 }
 
+// ---- ranks 5..8: the same one-workgroup design with the factor rows in two groups of four ----
+// Lane layout as k_solo_mu; w_[s][h] = W[gene(s)][4 h + j] (zero past the restart's rank kt).  G = W^T A runs two
+// 4x4x4 MFMA chains per (gene step, column group) -- rows 0..3 and 4..7 -- and W^T W three (rows 0-3 x 0-3,
+// 0-3 x 4-7, 4-7 x 4-7; the fourth block is the transpose of the second, the same products in the same order).
+// The register file cannot hold A beside these accumulators, so the last SL gene steps of A live in LDS, and each
+// wave sums its four gene blocks b (lane bits 2..3, row rotations) before writing its partials: the LDS holds
+// 16 doubles per (wave, chain) instead of 64.  Per iteration: MFMA chains -> block sums -> LDS | barrier | wave
+// sums in order (one thread per entry) | barrier | H update | barrier | stop check (wave 0) + h h^T (three 4x4x4
+// chains over the 48 padded samples, every wave, into its own LDS copy), F = A h^T on the VALU by gene batches
+// of SB steps and row groups (a quad reduce-scatter: lane j ends with row 4 h + j), E = W0 (h h^T) from the old
+// W of the batch (both groups), the W rule.  Every order is a function of (m, n, k) only.
+constexpr int S8_CH = 3;   // W^T W chains
+
+template <int NCG>
+struct Solo8Smem {
+  double Gp[SOLO_W][2 * NCG + S8_CH][16];   // block-summed partials, [chain][4 i + j] (i: row, j: column of the block)
+  double Hc[2][SOLO_NCOLP][8];              // H by (sample, row), rows padded to 8: zero past k and n
+  double Hh[SOLO_W][8][8];                  // h h^T, each wave's own copy
+  double Gs[8][4 * NCG];                    // G = W^T A
+  double WW[8][8];                          // W^T W
+  int stop, reason;
+};
+
+// sum of the four gene blocks b (lane bits 2..3) by row rotations; lanes with b = 0 hold it
+__device__ __forceinline__ double bsum4(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)(u & 0xffffffffLL), 0x124, 0xF, 0xF, true);   // row_ror:4
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0x124, 0xF, 0xF, true);
+  v += __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  const long long t = __double_as_longlong(v);
+  const int lo2 = __builtin_amdgcn_mov_dpp((int)(unsigned)(t & 0xffffffffLL), 0x128, 0xF, 0xF, true);  // row_ror:8
+  const int hi2 = __builtin_amdgcn_mov_dpp((int)(t >> 32), 0x128, 0xF, 0xF, true);
+  return v + __longlong_as_double((long long)(((unsigned long long)(unsigned)hi2 << 32) | (unsigned)lo2));
+}
+
+// quad reduce-scatter: lane j of the quad gets p[j] summed over the quad as (x_j + x_{j^2}) + (x_{j^1} + x_{j^3})
+__device__ __forceinline__ double qscatter4(const double (&p)[4], int j) {
+  const bool lo = j < 2, odd = j & 1;
+  const double r1 = qdpp<0x4E>(lo ? p[2] : p[0]);   // from lane j ^ 2
+  const double r2 = qdpp<0x4E>(lo ? p[3] : p[1]);
+  const double u1 = (lo ? p[0] : p[2]) + r1, u2 = (lo ? p[1] : p[3]) + r2;
+  const double r3 = qdpp<0xB1>(odd ? u1 : u2);      // from lane j ^ 1
+  return (odd ? u2 : u1) + r3;
+}
+
+template <int NCG, int SL, bool JOBS>
+__global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restrict__ A, int m, int n,
+                                                          double* __restrict__ W, double* __restrict__ H, int maxiter,
+                                                          int stop_rule, int* __restrict__ state, int kt_arg,
+                                                          SoloLayout lay) {
+  constexpr int SB = 4;                 // gene steps per F batch
+  constexpr int SR = SOLO_S - SL;       // gene steps of A in registers
+  __shared__ Solo8Smem<NCG> sm;
+  __shared__ double Al[SL > 0 ? SL : 1][NCG][64 * SOLO_W];
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, K = l >> 4,
+            bq = (l >> 2) & 3, j = l & 3;
+  double a_[SR > 0 ? SR : 1][NCG], w_[SOLO_S][2];
+  auto av = [&](int s, int cg) -> double { return s < SR ? a_[s < SR ? s : 0][cg] : Al[s < SR ? 0 : s - SR][cg][tid]; };
+#pragma unroll
+  for (int s = 0; s < SOLO_S; ++s) {
+    const int g = 128 * w + 16 * s + 4 * bq + K;
+#pragma unroll
+    for (int cg = 0; cg < NCG; ++cg) {
+      const int c = 4 * cg + j;
+      const double v = (g < m && c < n) ? A[(long)c * lay.a_ld + g] : 0.0;
+      if (s < SR)
+        a_[s < SR ? s : 0][cg] = v;
+      else
+        Al[s < SR ? 0 : s - SR][cg][tid] = v;
+    }
+  }
+  const int njobs = JOBS ? lay.njobs : 1;
+  for (int jx = JOBS ? (int)blockIdx.x : 0; jx < njobs; jx += JOBS ? (int)gridDim.x : 1) {
+  double* __restrict__ Wj = W;
+  double* __restrict__ Hj = H;
+  int kt = kt_arg, rid = -1;
+  if constexpr (JOBS) {   // uniform job fields (scalar registers: the vector ones are A's)
+    const nmfc::SoloJob jb = lay.jobs[__builtin_amdgcn_readfirstlane(jx)];
+    const int col0 = __builtin_amdgcn_readfirstlane(jb.col0);
+    Wj = W + (long)col0 * lay.w_ld;
+    Hj = H + (long)col0 * lay.h_sa;
+    kt = __builtin_amdgcn_readfirstlane(jb.k);
+    rid = __builtin_amdgcn_readfirstlane(jb.rid);
+  }
+#pragma unroll
+  for (int s = 0; s < SOLO_S; ++s) {
+    const int g = 128 * w + 16 * s + 4 * bq + K;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) w_[s][h] = (g < m && 4 * h + j < kt) ? Wj[(long)(4 * h + j) * lay.w_ld + g] : 0.0;
+  }
+  __syncthreads();   // the previous job's last reads of sm are done
+  for (int x = tid; x < 2 * SOLO_NCOLP * 8; x += 64 * SOLO_W) (&sm.Hc[0][0][0])[x] = 0.0;
+  if (tid == 0) {
+    sm.stop = 0;
+    sm.reason = 0;
+  }
+  __syncthreads();
+  for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
+    const int c = x / kt, a = x - c * kt;
+    sm.Hc[0][c][a] = Hj[(long)c * lay.h_sc + (long)a * lay.h_sa];
+  }
+  __syncthreads();
+  int hb = 0;
+  int cls = 0, unch = 0;   // wave 0: lane i's class, unchanged checks
+  for (int iter = 1; maxiter >= 1 && iter <= maxiter + 1; ++iter) {
+    // ---- this wave's partials of G = W^T A and W^T W (MFMA chains in gene order), gene blocks summed; the
+    // column groups in two passes over the gene steps (half the accumulators live at a time) ----
+    const int slot = 4 * K + j;   // D layout: lane 16 i + 4 b + j holds block b's [i][j]
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      constexpr int NH = (NCG + 1) / 2;
+      const int cg0 = part * NH, cg1 = part ? NCG : NH;
+      double acc[2][NH], ww[S8_CH];
+#pragma unroll
+      for (int c = 0; c < NH; ++c) acc[0][c] = acc[1][c] = 0.0;
+#pragma unroll
+      for (int c = 0; c < S8_CH; ++c) ww[c] = 0.0;
+#pragma unroll
+      for (int s = 0; s < SOLO_S; ++s) {
+#pragma unroll
+        for (int cg = cg0; cg < cg1; ++cg) {
+          const double x = av(s, cg);
+          acc[0][cg - cg0] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s][0], x, acc[0][cg - cg0], 0, 0, 0);
+          acc[1][cg - cg0] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s][1], x, acc[1][cg - cg0], 0, 0, 0);
+        }
+        if (part == 0) {
+          ww[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s][0], w_[s][0], ww[0], 0, 0, 0);
+          ww[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s][0], w_[s][1], ww[1], 0, 0, 0);
+          ww[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(w_[s][1], w_[s][1], ww[2], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int cg = cg0; cg < cg1; ++cg) {
+          const double v = bsum4(acc[h][cg - cg0]);
+          if (bq == 0) sm.Gp[w][h * NCG + cg][slot] = v;
+        }
+      if (part == 0) {
+#pragma unroll
+        for (int c = 0; c < S8_CH; ++c) {
+          const double v = bsum4(ww[c]);
+          if (bq == 0) sm.Gp[w][2 * NCG + c][slot] = v;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    if (sm.stop) break;   // decided at the previous iteration (its updates are done)
+    // ---- sums over the waves in order: G (kt x n) and W^T W (kt x kt), one thread per entry ----
+    // (tid through an empty asm: the index arithmetic of this phase, the H update and the stop check stays in
+    // its phase instead of being hoisted out of the iteration loop into registers A needs)
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    for (int o = tq; o < kt * n + kt * kt; o += 64 * SOLO_W) {
+      int ch, idx, a, c;
+      if (o < kt * n) {
+        a = o / n;
+        c = o - a * n;
+        ch = (a >> 2) * NCG + (c >> 2);
+        idx = 4 * (a & 3) + (c & 3);
+      } else {
+        a = (o - kt * n) / kt;
+        c = (o - kt * n) - a * kt;
+        const int ha = a >> 2, hc = c >> 2;
+        ch = 2 * NCG + ha + hc;
+        idx = ha > hc ? 4 * (c & 3) + (a & 3) : 4 * (a & 3) + (c & 3);   // rows 4-7 x 0-3: the transpose
+      }
+      double v = sm.Gp[0][ch][idx];
+#pragma unroll
+      for (int q = 1; q < SOLO_W; ++q) v += sm.Gp[q][ch][idx];
+      if (o < kt * n)
+        sm.Gs[a][c] = v;
+      else
+        sm.WW[a][c] = v;
+    }
+    __syncthreads();
+    // ---- H update (nmf_mu.c:178-191): d = (W^T W) H summed over the rows in order ----
+    const int nb = hb ^ 1;
+    asm volatile("" : "+v"(tq));
+    for (int x = tq; x < kt * n; x += 64 * SOLO_W) {
+      const int c = x / kt, a = x - c * kt;
+      double d = 0.0;
+      for (int b = 0; b < kt; ++b) d = fma(sm.WW[a][b], sm.Hc[hb][c][b], d);
+      sm.Hc[nb][c][a] = mu_rule(sm.Hc[hb][c][a], sm.Gs[a][c], d);
+    }
+    __syncthreads();
+    hb = nb;
+    // ---- stop rule (nmf_mu.c:253-282), wave 0 ----
+    if (w == 0) {
+      const bool check = stop_rule != nmfc::STOP_FIXED && iter > 1 && (iter % 2 == 0);
+      int reason = 0;
+      if (check) {
+        bool ch = false;
+        int lq = l;
+        asm volatile("" : "+v"(lq));   // window addresses computed here, not held across the loop
+        if (stop_rule == nmfc::STOP_REF_COMPAT) {
+          if (lq < kt && lq < n) {   // window i reads the flat k x n column-major buffer at [i n, i n + k)
+            int cl = 0;
+            double prev = 0.0;
+            for (int jj = 0; jj < kt; ++jj) {
+              const int f = lq * n + jj, c = f / kt, a = f - c * kt;
+              const double v = sm.Hc[hb][c][a];
+              if (jj > 0 && v > prev) cl = jj;
+              prev = v;
+            }
+            ch = cl != cls;
+            cls = cl;
+          }
+        } else if (stop_rule == nmfc::STOP_ARGMAX_STABLE) {
+          if (lq < n) {
+            int best = 0;
+            double bv = sm.Hc[hb][lq][0];
+            for (int a = 1; a < kt; ++a) {
+              const double v = sm.Hc[hb][lq][a];
+              if (v > bv) {
+                bv = v;
+                best = a;
+              }
+            }
+            ch = best != cls;
+            cls = best;
+          }
+        }
+        if (__ballot(ch) == 0) {
+          if (++unch >= 200) reason = 1;   // nmf_mu.c:269-271
+        } else {
+          unch = 0;
+        }
+      }
+      if (!reason && iter >= maxiter) reason = 2;
+      if (reason && l == 0) {
+        sm.stop = iter;
+        sm.reason = reason;
+      }
+    }
+    // ---- h h^T: three 4x4x4 chains over the padded samples (sample blocks b summed), into this wave's copy ----
+    {
+      int lq = l;
+      asm volatile("" : "+v"(lq));
+      const int hrow0 = 4 * ((lq >> 2) & 3) + (lq >> 4), hj = lq & 3;
+      double hll = 0.0, hlh = 0.0, hhh = 0.0;
+#pragma unroll
+      for (int t = 0; t < SOLO_NCOLP / 16; ++t) {
+        const double x0 = sm.Hc[hb][16 * t + hrow0][hj], x1 = sm.Hc[hb][16 * t + hrow0][4 + hj];
+        hll = __builtin_amdgcn_mfma_f64_4x4x4f64(x0, x0, hll, 0, 0, 0);
+        hlh = __builtin_amdgcn_mfma_f64_4x4x4f64(x0, x1, hlh, 0, 0, 0);
+        hhh = __builtin_amdgcn_mfma_f64_4x4x4f64(x1, x1, hhh, 0, 0, 0);
+      }
+      hll = bsum4(hll);
+      hlh = bsum4(hlh);
+      hhh = bsum4(hhh);
+      if (bq == 0) {   // lane 16 i + j: [i][j] of each block; rows 4-7 x 0-3 the transpose of rows 0-3 x 4-7
+        sm.Hh[w][K][j] = hll;
+        sm.Hh[w][K][4 + j] = hlh;
+        sm.Hh[w][4 + j][K] = hlh;
+        sm.Hh[w][4 + K][4 + j] = hhh;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // ---- F = A h^T (lane: samples 4 cg + j, then the quad), E = W0 (h h^T) from the batch's old W, W rule ----
+    const double* const hrow = &sm.Hc[hb][j][0];   // H[a][4 cg + j] at hrow[32 cg + a]
+    const double* const hhw = &sm.Hh[w][0][0];
+#pragma unroll
+    for (int s0 = 0; s0 < SOLO_S; s0 += SB) {
+      double e[2][SB], wn0[SB];
+      asm volatile("" ::: "memory");   // re-read H per batch: holding all of it would spill A
+      // E = W0 (h h^T) for both row groups from the batch's old W (W0[gene][b] from quad lane b & 3)
+      {
+        double hs0[8], hs1[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          hs0[b] = hhw[8 * b + j];
+          hs1[b] = hhw[8 * b + 4 + j];
+        }
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+          double e0 = 0.0, ee = 0.0;
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            const double bc = qbcast(w_[s0 + q][b >> 2], b & 3);
+            e0 = fma(bc, hs0[b], e0);
+            ee = fma(bc, hs1[b], ee);
+          }
+          e[0][q] = e0;
+          e[1][q] = ee;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double P[SB][4], hv[4], hn[4];   // the next column group's H loaded one group ahead
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hv[r] = hrow[4 * h + r];
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) {
+          if (cg + 1 < NCG) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hn[r] = hrow[32 * (cg + 1) + 4 * h + r];
+          }
+#pragma unroll
+          for (int q = 0; q < SB; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              P[q][r] = cg == 0 ? av(s0 + q, 0) * hv[r] : fma(av(s0 + q, cg), hv[r], P[q][r]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hv[r] = hn[r];
+        }
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+          const int s = s0 + q;
+          const double f = qscatter4(P[q], j);   // F[gene][4 h + j]
+          if (h == 0) {
+            wn0[q] = mu_rule_nb(w_[s][0], f, e[0][q]);
+          } else {
+            w_[s][1] = mu_rule_nb(w_[s][1], f, e[1][q]);
+            w_[s][0] = wn0[q];
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  // ---- final factors and the stop state ----
+#pragma unroll
+  for (int s = 0; s < SOLO_S; ++s) {
+    const int g = 128 * w + 16 * s + 4 * bq + K;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (g < m && 4 * h + j < kt) Wj[(long)(4 * h + j) * lay.w_ld + g] = w_[s][h];
+  }
+  for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
+    const int c = x / kt, a = x - c * kt;
+    Hj[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][a];
+  }
+  if (tid == 0) {
+    if constexpr (JOBS) {
+      lay.stop_iter[rid] = sm.stop;
+      lay.stop_reason[rid] = sm.reason;
+    } else {
+      state[0] = sm.stop;
+      state[1] = sm.reason;
+    }
+  }
+  }   // jobs
+}
+
+template <int NCG, int SL>
+hipError_t launch8(int grid, const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule, int* st,
+                   int kt, const SoloLayout& lay, hipStream_t s) {
+  if (lay.jobs)
+    hipLaunchKernelGGL((k_solo8_mu<NCG, SL, true>), dim3(grid), dim3(64 * SOLO_W), 0, s, A, m, n, W, H, maxiter,
+                       stop_rule, st, kt, lay);
+  else
+    hipLaunchKernelGGL((k_solo8_mu<NCG, SL, false>), dim3(grid), dim3(64 * SOLO_W), 0, s, A, m, n, W, H, maxiter,
+                       stop_rule, st, kt, lay);
+  return hipGetLastError();
+}
+
 template <int NCG, int KK, int SL = 0>
 hipError_t launch(int grid, const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule, int* st,
                   int kt, const SoloLayout& lay, hipStream_t s) {
@@ -407,8 +769,9 @@ hipError_t launch(int grid, const double* A, int m, int n, double* W, double* H,
   return hipGetLastError();
 }
 
-// the kernel rank for (n, k): k = 3 beyond n = 32 runs as k = 4 with a zero padding row
-int solo_rank(int n, int k) { return (k == 3 && (n + 3) / 4 > 8) ? 4 : k; }
+// the kernel rank for (n, k): k = 3 beyond n = 32 runs as k = 4 with a zero padding row; ranks 5..8 run on
+// k_solo8_mu (the restart's own rank, zero rows past it)
+int solo_rank(int n, int k) { return k >= 5 ? 8 : (k == 3 && (n + 3) / 4 > 8) ? 4 : k; }
 
 // the (column groups, rank, A steps in LDS) instantiation for (n, kernel rank kp); grid workgroups
 hipError_t dispatch(int grid, int kp, const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule,
@@ -416,6 +779,14 @@ hipError_t dispatch(int grid, int kp, const double* A, int m, int n, double* W, 
   // samples in column groups of 4: NCG = 4, 6, 8, 10 groups (n <= 16, 24, 32, 40)
   const int ncg = (n + 3) / 4;
   const int gi = ncg <= 4 ? 0 : ncg <= 6 ? 1 : ncg <= 8 ? 2 : 3;
+  if (kp == 8) {   // ranks 5..8: A steps in LDS where the registers would not hold them beside the two row groups
+    switch (gi) {
+      case 0: return launch8<4, 0>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+      case 1: return launch8<6, 1>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+      case 2: return launch8<8, 2>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+      default: return launch8<10, 3>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
+    }
+  }
   switch (kp * 4 + gi) {
     case 8: return launch<4, 2>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
     case 9: return launch<6, 2>(grid, A, m, n, W, H, maxiter, stop_rule, st, kt, lay, s);
@@ -481,12 +852,13 @@ extern "C" void nmfc_solo_release() {
   cache_drop();
 }
 
-// every shape with 2 <= k <= 4, k <= m <= 1024, k <= n <= 40.  Kernels by (k, column groups of 4 samples):
+// every shape with 2 <= k <= 8, k <= m <= 1024, k <= n <= 40 (ranks 5..8 on k_solo8_mu, A's last one to three
+// gene steps in LDS by n).  Ranks 2..4 by (k, column groups of 4 samples):
 // A fully in registers where that does not spill (k = 2; k = 3 to n = 32; k = 4 to n = 24); else the last
 // steps of A in LDS (k = 4: one step to n = 32, two to n = 40) and k = 3 beyond n = 32 as k = 4 with a zero
 // padding row (the rows of a restart never mix, so its bits are those of the unpadded arithmetic)
 extern "C" int nmfc_mu_solo_fits(int m, int n, int k) {
-  return m >= k && n >= k && k >= 2 && k <= 4 && m <= SOLO_MMAX && n <= SOLO_NMAX;
+  return m >= k && n >= k && k >= 2 && k <= 8 && m <= SOLO_MMAX && n <= SOLO_NMAX;
 }
 
 namespace {
@@ -501,7 +873,7 @@ extern "C" int nmfc_mu_solo(const double* A, int m, int n, int k, int maxiter, i
                             const double* H0, double* W, double* H, int* iters, int* early) {
   if (!A || !W0 || !H0 || !W || !H || !nmfc_mu_solo_fits(m, n, k) || maxiter < 0 ||
       (stop_rule != NMFC_STOP_FIXED && stop_rule != NMFC_STOP_REF_COMPAT && stop_rule != NMFC_STOP_ARGMAX_STABLE)) {
-    nmfc_set_error("nmfc_mu_solo: bad arguments (needs 2 <= k <= 4, k <= m <= 1024, k <= n <= 40)");
+    nmfc_set_error("nmfc_mu_solo: bad arguments (needs 2 <= k <= 8, k <= m <= 1024, k <= n <= 40)");
     return -1;
   }
   std::lock_guard<std::mutex> lock(g_lock);
@@ -587,7 +959,7 @@ __attribute__((visibility("hidden"))) int nmfc_solo_batch_launch(const double* A
                                                                  int maxiter, int stop_rule, int* stop_iter,
                                                                  int* stop_reason, int max_wgs, hipStream_t st) {
   if (njobs <= 0) return 0;
-  if (!nmfc_mu_solo_fits(m, n, 2) || kp < 2 || kp > 4) {
+  if (!nmfc_mu_solo_fits(m, n, 2) || kp < 2 || (kp > 4 && kp != 8)) {
     nmfc_set_error("nmfc_solo_batch_launch: shape outside the solo kernel's range");
     return -1;
   }

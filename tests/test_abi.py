@@ -181,8 +181,10 @@ def test_solo_path_shape_limits():
     import ctypes
     from nmfconsensus_amd import _lib
     L = _lib.lib()   # no device work: the range check comes first
-    assert L.nmfc_mu_solo_fits(1000, 40, 2) and L.nmfc_mu_solo_fits(1024, 40, 3) and L.nmfc_mu_solo_fits(1000, 40, 4)
-    for m, n, k in ((1000, 41, 2), (1025, 40, 2), (1000, 41, 3), (1000, 41, 4), (1000, 40, 5), (1000, 40, 1), (3, 2, 3)):
+    for m, n, k in ((1000, 40, 2), (1024, 40, 3), (1000, 40, 4), (1000, 40, 5), (1024, 40, 8), (8, 8, 8)):
+        assert L.nmfc_mu_solo_fits(m, n, k), (m, n, k)
+    for m, n, k in ((1000, 41, 2), (1025, 40, 2), (1000, 41, 3), (1000, 41, 4), (1000, 40, 9), (1000, 41, 8),
+                    (1025, 40, 6), (1000, 40, 1), (3, 2, 3), (7, 40, 8)):
         assert not L.nmfc_mu_solo_fits(m, n, k), (m, n, k)
     dp = ctypes.POINTER(ctypes.c_double)
     A = np.ones((1000, 41), order="F")

@@ -388,16 +388,17 @@ def test_c1_runif_sweep_vs_reference(gct_engine, golden_c2, rule, key):
 def test_c2_sweep_vs_reference(golden_c2, rule, key, kernel, monkeypatch):
     """BASELINE configs[1] (C2): synthetic 1000 x 40, k = 2..8, R = 100 (700 jobs) in one sweep against the
     reference's own nmf_mu run job by job: exits, labels, counts and consensus bit-exact; H within 1e-9.
-    kernel "auto": rank 2..4 on the one-workgroup solo kernel (one restart per workgroup), rank 5..8 on the
-    one-workgroup-per-block kernel, concurrently; "nosolo" (NMFC_SOLO=0) every rank on the block kernel; "team"
-    forces the team kernel for the blocks, whose teams then run ~10 blocks one after another (tag and buffer
-    continuity across blocks)."""
+    kernel "auto": every rank on the one-workgroup solo kernels (one restart per workgroup: k_solo_mu for rank
+    2..4, k_solo8_mu for 5..8, one launch per kernel rank, concurrently); "nosolo" (NMFC_SOLO=0) every rank on the
+    one-workgroup-per-block kernel; "team" (with NMFC_SOLO=0) forces the team kernel for the blocks, whose teams
+    then run ~10 blocks one after another (tag and buffer continuity across blocks)."""
     from nmfconsensus_amd.nmf import Engine
     g = golden_c2
     ks = [int(k) for k in g["c2_ks"]]
     R = int(g["c2_R"])
     if kernel == "team":
         monkeypatch.setenv("NMFC_SMALL_KERNEL", kernel)
+        monkeypatch.setenv("NMFC_SOLO", "0")
     elif kernel == "nosolo":
         monkeypatch.setenv("NMFC_SOLO", "0")
     with Engine(g["c2_A"]) as eng:
@@ -461,12 +462,13 @@ def test_block_packed_tail_bit_identical():
         assert np.array_equal(a.W[j], b.W[j]) and np.array_equal(a.H[j], b.H[j]), j
 
 
-@pytest.mark.parametrize("ks,R", [([2, 3, 4, 5], 5), ([4, 2], 3)])
+@pytest.mark.parametrize("ks,R", [([2, 3, 4, 5], 5), ([4, 2], 3), ([8, 6, 5, 7, 9], 3)])
 def test_solo_batch_bitidentical_to_drop_in(golden, oracle, ks, R):
-    """A sweep's rank 2..4 restarts run on the solo kernel, one workgroup each (batched launches beside k_small_mu):
-    every such job's W/H, exit and labels are bit-identical to the same job through the single-restart drop-in
-    (nmfc_mu_solo with the job's own generateMatrix(ran) init), so a job's bits do not depend on the batch.  The gct
-    has n = 40, so k = 3 runs padded to the 4-row kernel (its zero row never mixes in)."""
+    """A sweep's rank 2..8 restarts run on the solo kernels, one workgroup each (batched launches, one per kernel
+    rank, beside k_small_mu, which takes k = 9): every such job's W/H, exit and labels are bit-identical to the same
+    job through the single-restart drop-in (nmfc_mu_solo with the job's own generateMatrix(ran) init), so a job's
+    bits do not depend on the batch.  The gct has n = 40, so k = 3 runs padded to the 4-row kernel (its zero row
+    never mixes in); ranks 5..8 share one kernel (rows past k zero)."""
     import ctypes
     from nmfconsensus_amd import _lib
     from nmfconsensus_amd.nmf import Engine
@@ -491,7 +493,7 @@ def test_solo_batch_bitidentical_to_drop_in(golden, oracle, ks, R):
         assert r.iters[j] == it.value, (j, k)
         assert np.array_equal(r.W[j], W) and np.array_equal(r.H[j], H), (j, k)
         checked += 1
-    assert checked == sum(1 for j in range(len(ks) * R) if ks[j % len(ks)] <= 4)
+    assert checked == sum(1 for j in range(len(ks) * R) if ks[j % len(ks)] <= 8)
 
 
 def test_small_path_agrees_with_batched_engine(golden):
@@ -604,11 +606,14 @@ def test_nmf_mu_team_failure_falls_back(golden, monkeypatch):
 
 @pytest.mark.parametrize("m,n,k", [(1000, 40, 2), (1024, 37, 2), (1000, 32, 3), (700, 24, 4), (640, 16, 2),
                                    (37, 5, 4), (300, 29, 3), (129, 21, 4), (2, 9, 2),
-                                   (1000, 40, 3), (517, 37, 3), (1000, 40, 4), (1024, 30, 4), (3, 40, 3)])
+                                   (1000, 40, 3), (517, 37, 3), (1000, 40, 4), (1024, 30, 4), (3, 40, 3),
+                                   (1000, 40, 5), (1024, 40, 8), (1000, 37, 6), (700, 32, 7), (640, 24, 5),
+                                   (300, 16, 8), (129, 21, 6), (9, 8, 8), (37, 5, 5)])
 def test_solo_path_vs_oracle(oracle, m, n, k):
-    """nmf_mu on one workgroup (nmfc_mu_solo, csrc/solo.hip: rank 2..4 on gct-sized matrices, A in one CU's
-    registers, its last gene steps in LDS for k = 4 at n > 24, k = 3 at n > 32 run padded to 4 rows): fixed
-    counts within 1e-9, the REF_COMPAT and ARGMAX_STABLE exits exact, ragged m and n."""
+    """nmf_mu on one workgroup (nmfc_mu_solo, csrc/solo.hip: rank 2..8 on gct-sized matrices, A in one CU's
+    registers, its last gene steps in LDS for k = 4 at n > 24 and for ranks 5..8 at n > 16, k = 3 at n > 32 run
+    padded to 4 rows, ranks 5..8 on the two-row-group kernel with zero rows past k): fixed counts within 1e-9, the
+    REF_COMPAT and ARGMAX_STABLE exits exact, ragged m and n, every column-group form (n <= 16 / 24 / 32 / 40)."""
     import ctypes
     from nmfconsensus_amd import _lib
     L = _lib.lib()
@@ -632,11 +637,13 @@ def test_solo_path_vs_oracle(oracle, m, n, k):
 
 
 @pytest.mark.parametrize("m,n", [(200, 40), (500, 24), (700, 33), (1000, 64), (300, 16)])
-def test_small_kernel_wave_forms_vs_oracle(oracle, m, n):
+def test_small_kernel_wave_forms_vs_oracle(oracle, m, n, monkeypatch):
     """k_small_mu runs eight waves where m_pad is a multiple of 256 (m = 200 / 500 / 700 / 1000: 2 / 4 / 6 / 8 gene
-    blocks per wave) and four otherwise (m = 300 -> m_pad 384): rank 5..8 restarts (not the solo kernel's) in batches
-    against the oracle -- fixed counts within 1e-9, and the REF_COMPAT exits exact."""
+    blocks per wave) and four otherwise (m = 300 -> m_pad 384): rank 5..8 restarts in batches (NMFC_SOLO=0: the
+    solo kernel would take those with n <= 40) against the oracle -- fixed counts within 1e-9, and the REF_COMPAT
+    exits exact."""
     from nmfconsensus_amd.nmf import Engine
+    monkeypatch.setenv("NMFC_SOLO", "0")
     rng = np.random.default_rng(31 * m + n)
     A = np.asfortranarray(rng.random((m, n)) * 2.0 + 0.05)
     ks, R, T = [5, 6, 8], 2, 24
