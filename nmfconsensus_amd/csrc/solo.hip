@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/nmfc.h"
@@ -440,7 +441,9 @@ __device__ __forceinline__ double qscatter4(const double (&p)[4], int j) {
   return (odd ? u2 : u1) + r3;
 }
 
-template <int NCG, int SL, bool JOBS>
+// SKIP != 0 only in tools/solobench.hip (phase costs): bit 0 no G / W^T W MFMAs, 1 no F / E / W rule, 2 no h h^T,
+// 3 no stop check, 4 no wave sums, 5 no H update
+template <int NCG, int SL, bool JOBS, int SKIP = 0>
 __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restrict__ A, int m, int n,
                                                           double* __restrict__ W, double* __restrict__ H, int maxiter,
                                                           int stop_rule, int* __restrict__ state, int kt_arg,
@@ -485,6 +488,10 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
 #pragma unroll
     for (int h = 0; h < 2; ++h) w_[s][h] = (g < m && 4 * h + j < kt) ? Wj[(long)(4 * h + j) * lay.w_ld + g] : 0.0;
   }
+  // H in LDS by sample c, each row group of four rotated by c: row a at position (a & 4) | ((a - c) & 3), so lane j
+  // (samples c = j mod 4) finds row (j + r) & 3 of a group at position r (the F phase's rotated accumulation with
+  // uniform LDS offsets)
+  auto hp = [&](int c, int a) -> int { return (a & 4) | ((a - c) & 3); };
   __syncthreads();   // the previous job's last reads of sm are done
   for (int x = tid; x < 2 * SOLO_NCOLP * 8; x += 64 * SOLO_W) (&sm.Hc[0][0][0])[x] = 0.0;
   if (tid == 0) {
@@ -494,7 +501,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
   __syncthreads();
   for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
     const int c = x / kt, a = x - c * kt;
-    sm.Hc[0][c][a] = Hj[(long)c * lay.h_sc + (long)a * lay.h_sa];
+    sm.Hc[0][c][hp(c, a)] = Hj[(long)c * lay.h_sc + (long)a * lay.h_sa];
   }
   __syncthreads();
   int hb = 0;
@@ -513,7 +520,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
 #pragma unroll
       for (int c = 0; c < S8_CH; ++c) ww[c] = 0.0;
 #pragma unroll
-      for (int s = 0; s < SOLO_S; ++s) {
+      for (int s = 0; s < ((SKIP & 1) ? 0 : SOLO_S); ++s) {
 #pragma unroll
         for (int cg = cg0; cg < cg1; ++cg) {
           const double x = av(s, cg);
@@ -549,7 +556,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
     // its phase instead of being hoisted out of the iteration loop into registers A needs)
     int tq = tid;
     asm volatile("" : "+v"(tq));
-    for (int o = tq; o < kt * n + kt * kt; o += 64 * SOLO_W) {
+    for (int o = tq; !(SKIP & 16) && o < kt * n + kt * kt; o += 64 * SOLO_W) {
       int ch, idx, a, c;
       if (o < kt * n) {
         a = o / n;
@@ -575,17 +582,17 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
     // ---- H update (nmf_mu.c:178-191): d = (W^T W) H summed over the rows in order ----
     const int nb = hb ^ 1;
     asm volatile("" : "+v"(tq));
-    for (int x = tq; x < kt * n; x += 64 * SOLO_W) {
+    for (int x = tq; !(SKIP & 32) && x < kt * n; x += 64 * SOLO_W) {
       const int c = x / kt, a = x - c * kt;
       double d = 0.0;
-      for (int b = 0; b < kt; ++b) d = fma(sm.WW[a][b], sm.Hc[hb][c][b], d);
-      sm.Hc[nb][c][a] = mu_rule(sm.Hc[hb][c][a], sm.Gs[a][c], d);
+      for (int b = 0; b < kt; ++b) d = fma(sm.WW[a][b], sm.Hc[hb][c][hp(c, b)], d);
+      sm.Hc[nb][c][hp(c, a)] = mu_rule(sm.Hc[hb][c][hp(c, a)], sm.Gs[a][c], d);
     }
     __syncthreads();
     hb = nb;
     // ---- stop rule (nmf_mu.c:253-282), wave 0 ----
     if (w == 0) {
-      const bool check = stop_rule != nmfc::STOP_FIXED && iter > 1 && (iter % 2 == 0);
+      const bool check = !(SKIP & 8) && stop_rule != nmfc::STOP_FIXED && iter > 1 && (iter % 2 == 0);
       int reason = 0;
       if (check) {
         bool ch = false;
@@ -597,7 +604,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
             double prev = 0.0;
             for (int jj = 0; jj < kt; ++jj) {
               const int f = lq * n + jj, c = f / kt, a = f - c * kt;
-              const double v = sm.Hc[hb][c][a];
+              const double v = sm.Hc[hb][c][hp(c, a)];
               if (jj > 0 && v > prev) cl = jj;
               prev = v;
             }
@@ -607,9 +614,9 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
         } else if (stop_rule == nmfc::STOP_ARGMAX_STABLE) {
           if (lq < n) {
             int best = 0;
-            double bv = sm.Hc[hb][lq][0];
+            double bv = sm.Hc[hb][lq][hp(lq, 0)];
             for (int a = 1; a < kt; ++a) {
-              const double v = sm.Hc[hb][lq][a];
+              const double v = sm.Hc[hb][lq][hp(lq, a)];
               if (v > bv) {
                 bv = v;
                 best = a;
@@ -638,8 +645,10 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
       const int hrow0 = 4 * ((lq >> 2) & 3) + (lq >> 4), hj = lq & 3;
       double hll = 0.0, hlh = 0.0, hhh = 0.0;
 #pragma unroll
-      for (int t = 0; t < SOLO_NCOLP / 16; ++t) {
-        const double x0 = sm.Hc[hb][16 * t + hrow0][hj], x1 = sm.Hc[hb][16 * t + hrow0][4 + hj];
+      for (int t = 0; t < ((SKIP & 4) ? 0 : SOLO_NCOLP / 16); ++t) {
+        // rows hj and 4 + hj of sample 16 t + hrow0 (= K mod 4)
+        const int p0 = (hj - hrow0) & 3;
+        const double x0 = sm.Hc[hb][16 * t + hrow0][p0], x1 = sm.Hc[hb][16 * t + hrow0][4 + p0];
         hll = __builtin_amdgcn_mfma_f64_4x4x4f64(x0, x0, hll, 0, 0, 0);
         hlh = __builtin_amdgcn_mfma_f64_4x4x4f64(x0, x1, hlh, 0, 0, 0);
         hhh = __builtin_amdgcn_mfma_f64_4x4x4f64(x1, x1, hhh, 0, 0, 0);
@@ -658,31 +667,40 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // ---- F = A h^T (lane: samples 4 cg + j, then the quad), E = W0 (h h^T) from the batch's old W, W rule ----
-    const double* const hrow = &sm.Hc[hb][j][0];   // H[a][4 cg + j] at hrow[32 cg + a]
-    const double* const hhw = &sm.Hh[w][0][0];
+    // Each row group of four is accumulated rotated by lane -- register r of lane j holds row (j + r) & 3 of the
+    // group, which the rotated H storage puts at LDS position r -- so its quad reduction is three uniform rotations,
+    // no selects: F[.][j] = (P0 + rot2 P2) + (rot1 P3 + rot3 P1).  E sums its terms in the same rotated order.
+    // (Rows past kt are zero in H and W: the second group's lanes j >= kt - 4 keep their zero W.)
+    const double* const hrow = &sm.Hc[hb][j][0];   // position p of sample 4 cg + j at hrow[32 cg + p]
+    const double* const hhw = &sm.Hh[w][0][0];     // (h h^T)[b][a] at hhw[8 b + a]
 #pragma unroll
-    for (int s0 = 0; s0 < SOLO_S; s0 += SB) {
+    for (int s0 = 0; s0 < ((SKIP & 2) ? 0 : SOLO_S); s0 += SB) {
       double e[2][SB], wn0[SB];
       asm volatile("" ::: "memory");   // re-read H per batch: holding all of it would spill A
-      // E = W0 (h h^T) for both row groups from the batch's old W (W0[gene][b] from quad lane b & 3)
       {
-        double hs0[8], hs1[8];
+        // (h h^T)[b][a] for this lane's rows a = j (g = 0) and 4 + j (g = 1), b = 4 h + ((j + r) & 3)
+        double hs[2][2][4];
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          hs0[b] = hhw[8 * b + j];
-          hs1[b] = hhw[8 * b + 4 + j];
-        }
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hs[g][h][r] = hhw[8 * (4 * h + ((j + r) & 3)) + 4 * g + j];
 #pragma unroll
         for (int q = 0; q < SB; ++q) {
-          double e0 = 0.0, ee = 0.0;
+          double v0 = 0.0, v1 = 0.0;
 #pragma unroll
-          for (int b = 0; b < 8; ++b) {
-            const double bc = qbcast(w_[s0 + q][b >> 2], b & 3);
-            e0 = fma(bc, hs0[b], e0);
-            ee = fma(bc, hs1[b], ee);
+          for (int h = 0; h < 2; ++h) {
+            const double x = w_[s0 + q][h];
+            const double bc[4] = {x, qdpp<0x39>(x), qdpp<0x4E>(x), qdpp<0x93>(x)};   // W0[gene][4 h + ((j + r) & 3)]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v0 = fma(bc[r], hs[0][h][r], v0);
+              v1 = fma(bc[r], hs[1][h][r], v1);
+            }
           }
-          e[0][q] = e0;
-          e[1][q] = ee;
+          e[0][q] = v0;
+          e[1][q] = v1;
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -709,7 +727,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
 #pragma unroll
         for (int q = 0; q < SB; ++q) {
           const int s = s0 + q;
-          const double f = qscatter4(P[q], j);   // F[gene][4 h + j]
+          const double f = (P[q][0] + qdpp<0x4E>(P[q][2])) + (qdpp<0x39>(P[q][3]) + qdpp<0x93>(P[q][1]));
           if (h == 0) {
             wn0[q] = mu_rule_nb(w_[s][0], f, e[0][q]);
           } else {
@@ -731,7 +749,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
   }
   for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
     const int c = x / kt, a = x - c * kt;
-    Hj[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][a];
+    Hj[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][hp(c, a)];
   }
   if (tid == 0) {
     if constexpr (JOBS) {

@@ -24,9 +24,9 @@ SOLO_SPILLS = {
     "k_solo_muILi10ELi2ELi0ELi0ELi0ELb1E": 24,   # the same, batched job loop (C1 / C2)
     "k_solo_muILi10ELi4ELi0ELi0ELi2ELb1E": 1,    # k = 4 x 40, two gene steps in LDS, batched
     "k_solo_muILi8ELi3ELi0ELi0ELi0ELb1E": 2,     # k = 3 x 32, batched
-    "k_solo8_muILi10ELi3ELb0E": 5,               # ranks 5..8 x 40 samples (loop invariants of the stop check)
-    "k_solo8_muILi10ELi3ELb1E": 17,              # the same, batched (job-level addresses)
-    "k_solo8_muILi8ELi2ELb1E": 4,                # ranks 5..8 x 32, batched
+    "k_solo8_muILi10ELi3ELb0E": 12,              # ranks 5..8 x 40 samples (A at the register file's edge)
+    "k_solo8_muILi10ELi3ELb1E": 23,              # the same, batched (job-level addresses)
+    "k_solo8_muILi8ELi2ELb1E": 6,                # ranks 5..8 x 32, batched
 }
 
 
