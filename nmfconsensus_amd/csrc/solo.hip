@@ -105,6 +105,11 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
   constexpr int SB = SBO ? SBO : KK == 2 ? 8 : 4;
   __shared__ SoloSmem<NCG> sm;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, K = l >> 4, bq = (l >> 2) & 3, j = l & 3;
+  // KK = 4: H in LDS by sample c with its rows rotated by c (row a at position (a - c) & 3), so lane j (samples
+  // c = j mod 4) finds row (j + r) & 3 at position r: the F accumulation is rotated by lane and its quad reduction
+  // needs no selects (as k_solo8_mu)
+  constexpr bool ROT = KK == 4;
+  auto hp = [](int c, int a) -> int { return ROT ? ((a - c) & 3) : a; };
   constexpr int SR = SOLO_S - SL;   // gene steps of A in registers
   __shared__ double Al[SL > 0 ? SL : 1][NCG][64 * SOLO_W];   // steps SR.. of A, lane-contiguous
   double a_[SR > 0 ? SR : 1][NCG], w_[SOLO_S];
@@ -152,7 +157,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
   __syncthreads();
   for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
     const int c = x / kt, a = x - c * kt;
-    sm.Hc[0][c][a] = Hj[(long)c * lay.h_sc + (long)a * lay.h_sa];
+    sm.Hc[0][c][hp(c, a)] = Hj[(long)c * lay.h_sc + (long)a * lay.h_sa];
   }
   __syncthreads();
   long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = 0;
@@ -223,8 +228,8 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
       const int c = x / KK, a = x - c * KK;
       double d = 0.0;
 #pragma unroll
-      for (int b = 0; b < KK; ++b) d = fma(sm.WW[a][b], sm.Hc[hb][c][b], d);
-      sm.Hc[nb][c][a] = mu_rule(sm.Hc[hb][c][a], sm.Gs[a][c], d);
+      for (int b = 0; b < KK; ++b) d = fma(sm.WW[a][b], sm.Hc[hb][c][hp(c, b)], d);
+      sm.Hc[nb][c][hp(c, a)] = mu_rule(sm.Hc[hb][c][hp(c, a)], sm.Gs[a][c], d);
     }
     __syncthreads();
     SOLO_STAMP(4);
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
             double prev = 0.0;
             for (int jj = 0; jj < kt; ++jj) {
               const int f = l * n + jj, c = f / kt, a = f - c * kt;
-              const double v = sm.Hc[hb][c][a];
+              const double v = sm.Hc[hb][c][hp(c, a)];
               if (jj > 0 && v > prev) cl = jj;
               prev = v;
             }
@@ -253,9 +258,9 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
         } else if (stop_rule == nmfc::STOP_ARGMAX_STABLE) {
           if (l < n) {
             int best = 0;
-            double bv = sm.Hc[hb][l][0];
+            double bv = sm.Hc[hb][l][hp(l, 0)];
             for (int a = 1; a < kt; ++a) {
-              const double v = sm.Hc[hb][l][a];
+              const double v = sm.Hc[hb][l][hp(l, a)];
               if (v > bv) {
                 bv = v;
                 best = a;
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
     double hh = 0.0;
 #pragma unroll
     for (int t = 0; t < ((SKIP & 4) ? 0 : SOLO_NCOLP / 16); ++t) {
-      const double x = sm.Hc[hb][16 * t + 4 * bq + K][j];
+      const double x = sm.Hc[hb][16 * t + 4 * bq + K][ROT ? ((j - K) & 3) : j];   // row j of the sample
       hh = __builtin_amdgcn_mfma_f64_4x4x4f64(x, x, hh, 0, 0, 0);
     }
     // blocks summed by DPP row rotations; only lanes with b = 0 are read below, where the order is
@@ -296,9 +301,10 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
       const int hi2 = __builtin_amdgcn_mov_dpp((int)(v >> 32), 0x128, 0xF, 0xF, true);
       hh += __longlong_as_double((long long)(((unsigned long long)(unsigned)hi2 << 32) | (unsigned)lo2));
     }
-    double hs[KK];   // (h h^T)[b][a], a = this lane's row (j; j & 1 when k = 2, two gene steps per pass)
+    double hs[KK];   // (h h^T)[b][a], a = this lane's row (j; j & 1 when k = 2, two gene steps per pass); rotated
+                     // (b = (j + r) & 3 at r) when KK = 4
 #pragma unroll
-    for (int b = 0; b < KK; ++b) hs[b] = __shfl(hh, 16 * b + (KK == 2 ? (j & 1) : j));
+    for (int b = 0; b < KK; ++b) hs[b] = __shfl(hh, 16 * (ROT ? ((j + b) & 3) : b) + (KK == 2 ? (j & 1) : j));
     // ---- F = A h^T (this lane's samples 4 cg + j in order, then the quad), E = W0 (h h^T), W rule; genes in
     // batches of SB steps (the H row block re-read from LDS per batch) to bound the live registers ----
     const double* const hrow = &sm.Hc[hb][j][0];   // H[a][4 cg + j] at hrow[16 cg + a]
@@ -354,17 +360,25 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
 #pragma unroll
         for (int q = 0; q < SB; ++q) {
           const int s = s0 + q;
-          double f = 0.0;
+          double f = 0.0, e = 0.0;
+          if constexpr (ROT) {
+            // register r of lane j holds row (j + r) & 3: the quad sum of row j by three uniform rotations
+            f = (P[q][0] + qdpp<0x4E>(P[q][2])) + (qdpp<0x39>(P[q][3]) + qdpp<0x93>(P[q][1]));
+            e = fma(w_[s], hs[0], e);
+            e = fma(qdpp<0x39>(w_[s]), hs[1], e);
+            e = fma(qdpp<0x4E>(w_[s]), hs[2], e);
+            e = fma(qdpp<0x93>(w_[s]), hs[3], e);
+          } else {
 #pragma unroll
-          for (int a = 0; a < KK; ++a) {
-            double v = P[q][a];
-            v = v + qdpp<0xB1>(v);   // lanes j ^ 1
-            v = v + qdpp<0x4E>(v);   // lanes j ^ 2
-            f = (j == a) ? v : f;
+            for (int a = 0; a < KK; ++a) {
+              double v = P[q][a];
+              v = v + qdpp<0xB1>(v);   // lanes j ^ 1
+              v = v + qdpp<0x4E>(v);   // lanes j ^ 2
+              f = (j == a) ? v : f;
+            }
+#pragma unroll
+            for (int b = 0; b < KK; ++b) e = fma(qbcast(w_[s], b), hs[b], e);
           }
-          double e = 0.0;
-#pragma unroll
-          for (int b = 0; b < KK; ++b) e = fma(qbcast(w_[s], b), hs[b], e);
           if (j < KK) w_[s] = mu_rule_nb(w_[s], f, e);
         }
       }
@@ -382,7 +396,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
   }
   for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
     const int c = x / kt, a = x - c * kt;
-    Hj[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][a];
+    Hj[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][hp(c, a)];
   }
   if (tid == 0) {
     if constexpr (JOBS) {
