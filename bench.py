@@ -454,9 +454,10 @@ def bench_c1(args, dev):
         roof = {"bound": "mfma", "kernel": "small_mu", "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
                 "frac_metric": "algorithmic fp64 TFLOP/s / 78.6 TF", "frac_metric_version": 1,
-                "note": "one persistent launch runs the whole sweep's MU loops (k_small_mu): algorithmic flop of all "
-                        "restart-iterations (4mnk + 4(m+n)k^2 each) / its HIP-event duration; latency-bound (the "
-                        "longest 16-column block sets the launch), SURVEY 8(d): C1/C2 fit in L2"}
+                "note": "the small-shape phase (every restart's whole MU loop in one launch per kernel: k_solo_mu / "
+                        "k_solo8_mu one workgroup per restart at m <= 1024, n <= 40, ranks 2..8; k_small_mu blocks "
+                        "otherwise): algorithmic flop of all restart-iterations (4mnk + 4(m+n)k^2 each) / the phase's "
+                        "HIP-event duration; latency-bound (the longest restart sets it), SURVEY 8(d): C1/C2 fit in L2"}
     init = eng.run(ks, R, maxiter=0, seed=seed, want_factors=True, want_counts=False)
     eng.close()
     its = np.asarray(res.iters)

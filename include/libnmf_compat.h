@@ -52,7 +52,8 @@ typedef struct options_t {
  * REF_COMPAT form.  Returns 0, or -1 on allocation / device failure (nmf_mu.c:138-151).
  * Ranks: 1 <= k <= min(m, n).  Routing, a function of (m, n, k) only (so a restart gives the same bits on every call):
  *   solo    k = 2..4 on gct-sized matrices (nmfc_mu_solo_fits: m <= 1024, n <= 40): ONE workgroup runs the whole
- *           restart, A resident in its register file (csrc/solo.hip, k_solo_mu);
+ *           restart, A resident in its register file (csrc/solo.hip, k_solo_mu; ranks 5..8 have a one-workgroup
+ *           kernel too, k_solo8_mu, which batches use, but one call runs faster on a team);
  *   team    other k = 2..16 with m_pad = 128-rounded m <= 8192, n <= 64: a team of m_pad / 64 workgroups
  *           (k_team_mu, one launch with one upload / download);
  *   engine  other k = 2..16: the batched MFMA engine with a batch of one;

@@ -178,9 +178,11 @@ double nmf_mu(double* a, double* w0, double* h0, int* pm, int* pn, int* pk, int*
     printf("Exiting nmf_mu after %i\n", printed);
     return 0;
   }
-  // small rank on a gct-sized matrix: one workgroup runs the whole restart (csrc/solo.hip); NMFC_SOLO=0 disables
+  // rank 2..4 on a gct-sized matrix: one workgroup runs the whole restart (csrc/solo.hip); NMFC_SOLO=0 disables.
+  // Ranks 5..8 take the team below for ONE call (7.6 vs 11.5 us per iteration at k = 5 on the gct: sixteen CUs'
+  // latency against one CU's); a batch runs them on k_solo8_mu, one CU per restart, which carries more restarts.
   const char* solo_env = getenv("NMFC_SOLO");
-  if (nmfc_mu_solo_fits(m, n, k) && !(solo_env && atoi(solo_env) == 0)) {
+  if (k <= 4 && nmfc_mu_solo_fits(m, n, k) && !(solo_env && atoi(solo_env) == 0)) {
     int iters = 0, early = 0;
     if (nmfc_mu_solo(a, m, n, k, *maxiter, NMFC_STOP_REF_COMPAT, w0, h0, w0, h0, &iters, &early) != 0) {
       fprintf(stderr, "Error in nmf_mu: %s\n", nmfc_last_error());
