@@ -28,8 +28,12 @@ def main():
     out = {"shape": f"{m}x{n}", "maxiter": 10000, "reps": reps, "k": {}}
     devnull = os.open(os.devnull, os.O_WRONLY)
     saved = os.dup(1)
-    for k in (2, 5):   # first calls: HIP runtime + code objects, the solo path (k = 2) and the team engine (k = 5)
-        libnmf.nmf_mu(A, *ref.generate_ran(1, m, n, k), 10)
+    os.dup2(devnull, 1)   # the warm-up calls print "Exiting nmf_mu after ..." too: stdout holds only the JSON line
+    try:
+        for k in (2, 5):   # first calls: HIP runtime + code objects, the solo path (k = 2) and the team engine (k = 5)
+            libnmf.nmf_mu(A, *ref.generate_ran(1, m, n, k), 10)
+    finally:
+        os.dup2(saved, 1)
     for k in (2, 3, 4, 5):
         W0, H0 = ref.generate_ran(123, m, n, k)
         os.dup2(devnull, 1)   # both print "Exiting nmf_mu after ..." (nmf_mu.c:296)
