@@ -416,11 +416,14 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
 // 0-3 x 4-7, 4-7 x 4-7; the fourth block is the transpose of the second, the same products in the same order).
 // The register file cannot hold A beside these accumulators, so the last SL gene steps of A live in LDS, and each
 // wave sums its four gene blocks b (lane bits 2..3, row rotations) before writing its partials: the LDS holds
-// 16 doubles per (wave, chain) instead of 64.  Per iteration: MFMA chains -> block sums -> LDS | barrier | wave
-// sums in order (one thread per entry) | barrier | H update | barrier | stop check (wave 0) + h h^T (three 4x4x4
-// chains over the 48 padded samples, every wave, into its own LDS copy), F = A h^T on the VALU by gene batches
-// of SB steps and row groups (a quad reduce-scatter: lane j ends with row 4 h + j), E = W0 (h h^T) from the old
-// W of the batch (both groups), the W rule.  Every order is a function of (m, n, k) only.
+// 16 doubles per (wave, chain) instead of 64.  F = A h^T and E = W0 (h h^T) run on 4x4x4 MFMAs too: the X operand
+// is A's (W0's) block with the lane fields of gene and sample (factor) swapped -- a ds_bpermute for the steps in
+// registers, a permuted LDS address for those in LDS -- and D lands in W's own layout, so the W rule is elementwise
+// (a VALU form with quad reductions was 12 % slower: k-padding aside, its ~1 450 VALU instructions per lane per
+// iteration cost more than the 4x4x4 MFMAs at ~25 cycles each).  Per iteration: MFMA chains -> block sums -> LDS |
+// barrier | wave sums in order (one thread per entry) | barrier | H update | barrier | stop check (wave 0) + h h^T
+// (three 4x4x4 chains over the 48 padded samples, every wave, into its own LDS copy), F / E / W rule by gene
+// steps.  Every order is a function of (m, n, k) only.
 constexpr int S8_CH = 3;   // W^T W chains
 
 template <int NCG>
@@ -445,24 +448,13 @@ __device__ __forceinline__ double bsum4(double v) {
   return v + __longlong_as_double((long long)(((unsigned long long)(unsigned)hi2 << 32) | (unsigned)lo2));
 }
 
-// quad reduce-scatter: lane j of the quad gets p[j] summed over the quad as (x_j + x_{j^2}) + (x_{j^1} + x_{j^3})
-__device__ __forceinline__ double qscatter4(const double (&p)[4], int j) {
-  const bool lo = j < 2, odd = j & 1;
-  const double r1 = qdpp<0x4E>(lo ? p[2] : p[0]);   // from lane j ^ 2
-  const double r2 = qdpp<0x4E>(lo ? p[3] : p[1]);
-  const double u1 = (lo ? p[0] : p[2]) + r1, u2 = (lo ? p[1] : p[3]) + r2;
-  const double r3 = qdpp<0xB1>(odd ? u1 : u2);      // from lane j ^ 1
-  return (odd ? u2 : u1) + r3;
-}
-
 // SKIP != 0 only in tools/solobench.hip (phase costs): bit 0 no G / W^T W MFMAs, 1 no F / E / W rule, 2 no h h^T,
 // 3 no stop check, 4 no wave sums, 5 no H update
-template <int NCG, int SL, bool JOBS, int SKIP = 0>
+template <int NCG, int SL, bool JOBS, int SKIP = 0, int FMQ = JOBS ? 2 : 4>
 __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restrict__ A, int m, int n,
                                                           double* __restrict__ W, double* __restrict__ H, int maxiter,
                                                           int stop_rule, int* __restrict__ state, int kt_arg,
                                                           SoloLayout lay) {
-  constexpr int SB = 4;                 // gene steps per F batch
   constexpr int SR = SOLO_S - SL;       // gene steps of A in registers
   __shared__ Solo8Smem<NCG> sm;
   __shared__ double Al[SL > 0 ? SL : 1][NCG][64 * SOLO_W];
@@ -502,10 +494,6 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
 #pragma unroll
     for (int h = 0; h < 2; ++h) w_[s][h] = (g < m && 4 * h + j < kt) ? Wj[(long)(4 * h + j) * lay.w_ld + g] : 0.0;
   }
-  // H in LDS by sample c, each row group of four rotated by c: row a at position (a & 4) | ((a - c) & 3), so lane j
-  // (samples c = j mod 4) finds row (j + r) & 3 of a group at position r (the F phase's rotated accumulation with
-  // uniform LDS offsets)
-  auto hp = [&](int c, int a) -> int { return (a & 4) | ((a - c) & 3); };
   __syncthreads();   // the previous job's last reads of sm are done
   for (int x = tid; x < 2 * SOLO_NCOLP * 8; x += 64 * SOLO_W) (&sm.Hc[0][0][0])[x] = 0.0;
   if (tid == 0) {
@@ -515,7 +503,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
   __syncthreads();
   for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
     const int c = x / kt, a = x - c * kt;
-    sm.Hc[0][c][hp(c, a)] = Hj[(long)c * lay.h_sc + (long)a * lay.h_sa];
+    sm.Hc[0][c][a] = Hj[(long)c * lay.h_sc + (long)a * lay.h_sa];
   }
   __syncthreads();
   int hb = 0;
@@ -599,8 +587,8 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
     for (int x = tq; !(SKIP & 32) && x < kt * n; x += 64 * SOLO_W) {
       const int c = x / kt, a = x - c * kt;
       double d = 0.0;
-      for (int b = 0; b < kt; ++b) d = fma(sm.WW[a][b], sm.Hc[hb][c][hp(c, b)], d);
-      sm.Hc[nb][c][hp(c, a)] = mu_rule(sm.Hc[hb][c][hp(c, a)], sm.Gs[a][c], d);
+      for (int b = 0; b < kt; ++b) d = fma(sm.WW[a][b], sm.Hc[hb][c][b], d);
+      sm.Hc[nb][c][a] = mu_rule(sm.Hc[hb][c][a], sm.Gs[a][c], d);
     }
     __syncthreads();
     hb = nb;
@@ -618,7 +606,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
             double prev = 0.0;
             for (int jj = 0; jj < kt; ++jj) {
               const int f = lq * n + jj, c = f / kt, a = f - c * kt;
-              const double v = sm.Hc[hb][c][hp(c, a)];
+              const double v = sm.Hc[hb][c][a];
               if (jj > 0 && v > prev) cl = jj;
               prev = v;
             }
@@ -628,9 +616,9 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
         } else if (stop_rule == nmfc::STOP_ARGMAX_STABLE) {
           if (lq < n) {
             int best = 0;
-            double bv = sm.Hc[hb][lq][hp(lq, 0)];
+            double bv = sm.Hc[hb][lq][0];
             for (int a = 1; a < kt; ++a) {
-              const double v = sm.Hc[hb][lq][hp(lq, a)];
+              const double v = sm.Hc[hb][lq][a];
               if (v > bv) {
                 bv = v;
                 best = a;
@@ -660,9 +648,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
       double hll = 0.0, hlh = 0.0, hhh = 0.0;
 #pragma unroll
       for (int t = 0; t < ((SKIP & 4) ? 0 : SOLO_NCOLP / 16); ++t) {
-        // rows hj and 4 + hj of sample 16 t + hrow0 (= K mod 4)
-        const int p0 = (hj - hrow0) & 3;
-        const double x0 = sm.Hc[hb][16 * t + hrow0][p0], x1 = sm.Hc[hb][16 * t + hrow0][4 + p0];
+        const double x0 = sm.Hc[hb][16 * t + hrow0][hj], x1 = sm.Hc[hb][16 * t + hrow0][4 + hj];
         hll = __builtin_amdgcn_mfma_f64_4x4x4f64(x0, x0, hll, 0, 0, 0);
         hlh = __builtin_amdgcn_mfma_f64_4x4x4f64(x0, x1, hlh, 0, 0, 0);
         hhh = __builtin_amdgcn_mfma_f64_4x4x4f64(x1, x1, hhh, 0, 0, 0);
@@ -680,76 +666,58 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    // ---- F = A h^T (lane: samples 4 cg + j, then the quad), E = W0 (h h^T) from the batch's old W, W rule ----
-    // Each row group of four is accumulated rotated by lane -- register r of lane j holds row (j + r) & 3 of the
-    // group, which the rotated H storage puts at LDS position r -- so its quad reduction is three uniform rotations,
-    // no selects: F[.][j] = (P0 + rot2 P2) + (rot1 P3 + rot3 P1).  E sums its terms in the same rotated order.
-    // (Rows past kt are zero in H and W: the second group's lanes j >= kt - 4 keep their zero W.)
-    const double* const hrow = &sm.Hc[hb][j][0];   // position p of sample 4 cg + j at hrow[32 cg + p]
-    const double* const hhw = &sm.Hh[w][0][0];     // (h h^T)[b][a] at hhw[8 b + a]
+    {
+      // ---- F = A h^T and E = W0 (h h^T) on 4x4x4 MFMAs, W rule ----
+      // X = A's (gene, sample) block with the two lane fields swapped (lane 16 kk + 4 b + i takes the value of lane
+      // 16 i + 4 b + kk: ds_bpermute for the steps in registers, a permuted LDS address for those in LDS), Y = the
+      // H^T block; D lands in W's own layout (lane 16 K + 4 b + j: gene 16 s + 4 b + K, row 4 h + j), so the rule
+      // needs no reduction.  F chains over the column groups in order; E over the two row groups.
+      const int tl = ((l & 3) << 4) | (l & 12) | (l >> 4);
+      auto tperm = [&](double v) -> double {
+        const long long u = __double_as_longlong(v);
+        const int lo = __builtin_amdgcn_ds_bpermute(tl << 2, (int)(unsigned)(u & 0xffffffffLL));
+        const int hi = __builtin_amdgcn_ds_bpermute(tl << 2, (int)(u >> 32));
+        return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+      };
+      double Y[NCG][2], Yh[2][2];   // H[4 h + j][4 t + K]; (h h^T)[4 g + K][4 h + j]
 #pragma unroll
-    for (int s0 = 0; s0 < ((SKIP & 2) ? 0 : SOLO_S); s0 += SB) {
-      double e[2][SB], wn0[SB];
-      asm volatile("" ::: "memory");   // re-read H per batch: holding all of it would spill A
-      {
-        // (h h^T)[b][a] for this lane's rows a = j (g = 0) and 4 + j (g = 1), b = 4 h + ((j + r) & 3)
-        double hs[2][2][4];
+      for (int t = 0; t < NCG; ++t)
 #pragma unroll
-        for (int g = 0; g < 2; ++g)
+        for (int h = 0; h < 2; ++h) Y[t][h] = sm.Hc[hb][4 * t + K][4 * h + j];
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
+      for (int g = 0; g < 2; ++g)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) hs[g][h][r] = hhw[8 * (4 * h + ((j + r) & 3)) + 4 * g + j];
+        for (int h = 0; h < 2; ++h) Yh[g][h] = sm.Hh[w][4 * g + K][4 * h + j];
+      constexpr int SQ = FMQ;   // gene steps whose chains run interleaved
 #pragma unroll
-        for (int q = 0; q < SB; ++q) {
-          double v0 = 0.0, v1 = 0.0;
+      for (int s0 = 0; s0 < ((SKIP & 2) ? 0 : SOLO_S); s0 += SQ) {
+        double f[SQ][2], e[SQ][2];
+#pragma unroll
+        for (int q = 0; q < SQ; ++q) {
+          const double x0 = tperm(w_[s0 + q][0]), x1 = tperm(w_[s0 + q][1]);
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const double x = w_[s0 + q][h];
-            const double bc[4] = {x, qdpp<0x39>(x), qdpp<0x4E>(x), qdpp<0x93>(x)};   // W0[gene][4 h + ((j + r) & 3)]
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              v0 = fma(bc[r], hs[0][h][r], v0);
-              v1 = fma(bc[r], hs[1][h][r], v1);
-            }
+            e[q][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(x0, Yh[0][h], 0.0, 0, 0, 0);
+            e[q][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(x1, Yh[1][h], e[q][h], 0, 0, 0);
+            f[q][h] = 0.0;
           }
-          e[0][q] = v0;
-          e[1][q] = v1;
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        double P[SB][4], hv[4], hn[4];   // the next column group's H loaded one group ahead
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hv[r] = hrow[4 * h + r];
-#pragma unroll
-        for (int cg = 0; cg < NCG; ++cg) {
-          if (cg + 1 < NCG) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) hn[r] = hrow[32 * (cg + 1) + 4 * h + r];
-          }
-#pragma unroll
-          for (int q = 0; q < SB; ++q)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              P[q][r] = cg == 0 ? av(s0 + q, 0) * hv[r] : fma(av(s0 + q, cg), hv[r], P[q][r]);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) hv[r] = hn[r];
         }
 #pragma unroll
-        for (int q = 0; q < SB; ++q) {
+        for (int t = 0; t < NCG; ++t)
+#pragma unroll
+          for (int q = 0; q < SQ; ++q) {
+            const int s = s0 + q;
+            const double x = s < SR ? tperm(a_[s < SR ? s : 0][t]) : Al[s < SR ? 0 : s - SR][t][64 * w + tl];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) f[q][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(x, Y[t][h], f[q][h], 0, 0, 0);
+          }
+#pragma unroll
+        for (int q = 0; q < SQ; ++q) {
           const int s = s0 + q;
-          const double f = (P[q][0] + qdpp<0x4E>(P[q][2])) + (qdpp<0x39>(P[q][3]) + qdpp<0x93>(P[q][1]));
-          if (h == 0) {
-            wn0[q] = mu_rule_nb(w_[s][0], f, e[0][q]);
-          } else {
-            w_[s][1] = mu_rule_nb(w_[s][1], f, e[1][q]);
-            w_[s][0] = wn0[q];
-          }
+          const double n0 = mu_rule_nb(w_[s][0], f[q][0], e[q][0]);
+          w_[s][1] = mu_rule_nb(w_[s][1], f[q][1], e[q][1]);
+          w_[s][0] = n0;
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -763,7 +731,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
   }
   for (int x = tid; x < kt * n; x += 64 * SOLO_W) {
     const int c = x / kt, a = x - c * kt;
-    Hj[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][hp(c, a)];
+    Hj[(long)c * lay.h_sc + (long)a * lay.h_sa] = sm.Hc[hb][c][a];
   }
   if (tid == 0) {
     if constexpr (JOBS) {

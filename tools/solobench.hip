@@ -118,6 +118,8 @@ void bench8(int m, int n, int T, int kt) {
     printf("  %-30s %8.3f ms  %7.2f us/iteration  (ran %d)\n", name, best, best * 1e3 / hs[0], hs[0]);
   };
   run(k_solo8_mu<NCG, SL, false, 0>, "full");
+  run(k_solo8_mu<NCG, SL, false, 0, 1>, "full, one gene step per F pass");
+  run(k_solo8_mu<NCG, SL, false, 0, 2>, "full, two gene steps per F pass");
   run(k_solo8_mu<NCG, SL, false, 1>, "no G MFMA");
   run(k_solo8_mu<NCG, SL, false, 2>, "no F/E/W");
   run(k_solo8_mu<NCG, SL, false, 4>, "no h h^T");
