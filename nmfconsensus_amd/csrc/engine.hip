@@ -90,7 +90,7 @@ struct DevBuf {
   }
 };
 
-// 31x31 jump matrices J[c] = M^(c*RCHUNK) mod 2^32 of the recurrence r[i] = r[i-31] + r[i-3]
+// 31x31 jump matrices J[c] = M^(c * rchunk) mod 2^32 of the recurrence r[i] = r[i-31] + r[i-3]
 // acting on the ordered window (r[i-31], ..., r[i-1]).
 void mat_mul31(const uint32_t* A, const uint32_t* B, uint32_t* C) {
   for (int i = 0; i < 31; ++i)
@@ -101,14 +101,14 @@ void mat_mul31(const uint32_t* A, const uint32_t* B, uint32_t* C) {
     }
 }
 
-std::vector<uint32_t> make_jump_table(int nchunks) {
+std::vector<uint32_t> make_jump_table(int nchunks, int rchunk) {
   std::vector<uint32_t> M(31 * 31, 0), P(31 * 31, 0), T(31 * 31);
   for (int q = 0; q < 30; ++q) M[q * 31 + q + 1] = 1;
   M[30 * 31 + 0] = 1;    // r[i-31]
   M[30 * 31 + 28] += 1;  // r[i-3]
   for (int i = 0; i < 31; ++i) P[i * 31 + i] = 1;
   std::vector<uint32_t> base = M;
-  for (int e = RCHUNK; e > 0; e >>= 1) {   // P = M^RCHUNK
+  for (int e = rchunk; e > 0; e >>= 1) {   // P = M^rchunk
     if (e & 1) {
       mat_mul31(P.data(), base.data(), T.data());
       P = T;
@@ -340,7 +340,7 @@ struct nmfc_engine {
   size_t mu1_host_bytes = 0;
   int mu1_base = -1;   // -1: the flags must be zeroed
   int mu1_kprev = 16;  // staging rows [k, mu1_kprev) may hold a previous call's factors
-  int jump_chunks = 0;
+  int jump_chunks = 0, jump_rchunk = 0;   // the jump table on the device: chunks, draws per chunk
   int* h_stopped = nullptr;   // pinned, 2 slots
   // timing
   bool timing = false;
@@ -913,10 +913,16 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     std::vector<InitJob> ij(nj);
     std::vector<int> cj, ci;
     int maxch = 1;
+    // draws per thread: halve the chunk (down to 62) while the sweep would run fewer than 65 536 threads -- the
+    // draws of one chunk are a dependent sequence, and the jump product a thread starts with costs ~1 000 ops
+    long draws = 0;
+    for (int q = 0; q < nj; ++q) draws += (long)m * pk.ri[q].k + (long)pk.ri[q].k * n;
+    int rchunk = RCHUNK;
+    while (rchunk > 62 && draws / rchunk < 65536) rchunk /= 2;
     for (int q = 0; q < nj; ++q) {
       const RestartInfo& r = pk.ri[q];
       const long total = (long)m * r.k + (long)r.k * n;
-      const int nch = (int)((total + RCHUNK - 1) / RCHUNK);
+      const int nch = (int)((total + rchunk - 1) / rchunk);
       ij[q].seed = (uint32_t)(opts.seed + (uint32_t)(jb + rslot[r.rid]));   // job seed = seed + job_id - 1
       ij[q].col0 = r.col0;
       ij[q].k = r.k;
@@ -927,12 +933,13 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         ci.push_back(c);
       }
     }
-    if (maxch > e->jump_chunks) {
-      std::vector<uint32_t> tab = make_jump_table(maxch);
+    if (maxch > e->jump_chunks || rchunk != e->jump_rchunk) {
+      std::vector<uint32_t> tab = make_jump_table(maxch, rchunk);
       if (e->jump.ensure(sizeof(uint32_t) * tab.size())) return -1;
       HCHECK(hipMemcpyAsync(e->jump.p, tab.data(), sizeof(uint32_t) * tab.size(), hipMemcpyHostToDevice, st));
       HCHECK(hipStreamSynchronize(st));
       e->jump_chunks = maxch;
+      e->jump_rchunk = rchunk;
     }
     if (e->initjobs.ensure(sizeof(InitJob) * nj) || e->chunk_job.ensure(sizeof(int) * cj.size()) ||
         e->chunk_idx.ensure(sizeof(int) * ci.size()))
@@ -944,7 +951,8 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
     {
       TimedLaunch tl(e, KID_INIT);
       hipLaunchKernelGGL(k_init, dim3((total_chunks + NT - 1) / NT), dim3(NT), 0, st, e->initjobs.as<InitJob>(),
-                         e->chunk_job.as<int>(), e->chunk_idx.as<int>(), total_chunks, e->jump.as<uint32_t>(), m, n,
+                         e->chunk_job.as<int>(), e->chunk_idx.as<int>(), total_chunks, e->jump.as<uint32_t>(), rchunk / 31,
+                         m, n,
                          e->m_pad, e->n_pad, opts.min_init, opts.max_init, e->W[0].as<double>(), e->H[0].as<double>());
     }
     HCHECK(hipGetLastError());

@@ -2110,11 +2110,12 @@ static __global__ __launch_bounds__(NT) void k_move_rows(const MoveJob* __restri
 
 // ---------------------------------------------------------------------------------------------
 // Init: generateMatrix(ran) (generatematrix.c:131-137) with randnumber (randnumber.c:34) over the
-// glibc TYPE_3 stream seeded per job.  Thread = (restart, chunk of RCHUNK draws); the chunk's start
-// state is J[c] * s_344 (mod 2^32), J[c] = M^(c*RCHUNK) the 31x31 jump matrix of the lagged
-// recurrence r[i] = r[i-31] + r[i-3].
+// glibc TYPE_3 stream seeded per job.  Thread = (restart, chunk of 31 * rnb draws); the chunk's start
+// state is J[c] * s_344 (mod 2^32), J[c] = M^(c * 31 * rnb) the 31x31 jump matrix of the lagged
+// recurrence r[i] = r[i-31] + r[i-3].  The host picks rnb per run: long chunks (few jump products) when the
+// sweep has draws enough to fill the GPU, short ones when it has not (C1's 73 000 draws were 74 threads).
 // ---------------------------------------------------------------------------------------------
-constexpr int RCHUNK = 31 * 32;   // draws per thread (multiple of 31 for a statically indexed ring)
+constexpr int RCHUNK = 31 * 32;   // longest chunk: draws per thread (a multiple of 31: a statically indexed ring)
 
 struct InitJob {
   uint32_t seed;
@@ -2125,7 +2126,7 @@ struct InitJob {
 
 static __global__ __launch_bounds__(NT) void k_init(const InitJob* __restrict__ jobs, const int* __restrict__ chunk_job,
                                                     const int* __restrict__ chunk_idx, int total_chunks,
-                                                    const uint32_t* __restrict__ jump, int m, int n, long m_pad,
+                                                    const uint32_t* __restrict__ jump, int rnb, int m, int n, long m_pad,
                                                     long n_pad, int min_init, int max_init, double* __restrict__ W,
                                                     double* __restrict__ H) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2171,12 +2172,22 @@ static __global__ __launch_bounds__(NT) void k_init(const InitJob* __restrict__ 
 #pragma unroll
     for (int q = 0; q < 31; ++q) ring[q] = s[q];
   }
-  // ring[q] = r[i0 - 31 + q]; step jj overwrites slot jj % 31 with r[i0+jj] = slot + slot[(jj+28)%31]
-  const long mk = (long)m * jb.k;
-  const long total = mk + (long)jb.k * n;
-  long t = (long)c * RCHUNK;
+  // ring[q] = r[i0 - 31 + q]; step jj overwrites slot jj % 31 with r[i0+jj] = slot + slot[(jj+28)%31].
+  // Draw t goes to W (column-major m x k: row i, column a) while t < m k, then to H (k x n: row a, column jcol);
+  // both positions advance incrementally (one division per thread, not two 64-bit divisions per draw).
+  const int mk = m * jb.k;
+  const int total = mk + jb.k * n;
+  int t = c * 31 * rnb;
+  int p0, p1;   // (i, a) in W, then (a, jcol) in H
+  if (t < mk) {
+    p1 = t / m;
+    p0 = t - p1 * m;
+  } else {
+    p1 = (t - mk) / jb.k;
+    p0 = (t - mk) - p1 * jb.k;
+  }
 #pragma unroll 1
-  for (int blk = 0; blk < RCHUNK / 31; ++blk) {
+  for (int blk = 0; blk < rnb; ++blk) {
 #pragma unroll
     for (int q = 0; q < 31; ++q) {
       const uint32_t v = ring[q] + ring[(q + 28) % 31];
@@ -2186,12 +2197,17 @@ static __global__ __launch_bounds__(NT) void k_init(const InitJob* __restrict__ 
         const int32_t prod = (int32_t)((uint32_t)(max_init - min_init) * (uint32_t)o);
         const double val = (double)min_init + (double)prod / 2147483647.0;
         if (t < mk) {
-          const long a = t / m, i = t - a * m;
-          W[(long)(jb.col0 + a) * m_pad + i] = val;
+          W[(long)(jb.col0 + p1) * m_pad + p0] = val;
+          if (++p0 == m) {
+            p0 = 0;
+            if (++p1 == jb.k) p1 = 0;   // t + 1 == mk: H starts at (a, jcol) = (0, 0)
+          }
         } else {
-          const long tt = t - mk;
-          const long jcol = tt / jb.k, a = tt - jcol * jb.k;
-          H[(long)(jb.col0 + a) * n_pad + jcol] = val;
+          H[(long)(jb.col0 + p0) * n_pad + p1] = val;
+          if (++p0 == jb.k) {
+            p0 = 0;
+            ++p1;
+          }
         }
       }
       ++t;
