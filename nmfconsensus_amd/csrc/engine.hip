@@ -274,12 +274,15 @@ int live_panels(const Packing& pk) {
 
 // Small-shape path, restarts that the one-workgroup solo kernels take (nmfc_mu_solo_fits(m, n, k): rank <= 8 on
 // gct-sized shapes): each gets 4 (kernel rank <= 4) or 8 stacked columns of its own after the k_small_mu blocks
-// (cols from col_base), in order of kernel rank (one launch per rank), then restart id.  Returns the solo jobs; pk
-// grows to hold them.
+// (cols from col_base), in order of kernel rank (one launch per rank), then rank descending, then restart id.
+// Returns the solo jobs; pk grows to hold them.
 std::vector<SoloJob> place_solo(Packing& pk, std::vector<RestartInfo> solo, int col_base, int n) {
+  // within a kernel rank the higher ranks first (k_solo8_mu takes k = 5..8 at one cost per iteration, and higher
+  // ranks run longer on average: the dispatcher, which starts a launch's workgroups in order, then starts the likely
+  // stragglers first -- C2's 1 482-iteration k = 8 restart no longer waits for a free CU)
   std::stable_sort(solo.begin(), solo.end(), [n](const RestartInfo& a, const RestartInfo& b) {
     const int ka = nmfc_solo_batch_rank(n, a.k), kb = nmfc_solo_batch_rank(n, b.k);
-    return ka != kb ? ka < kb : a.rid < b.rid;
+    return ka != kb ? ka < kb : a.k != b.k ? a.k > b.k : a.rid < b.rid;
   });
   std::vector<SoloJob> jobs;
   int col = col_base;
