@@ -274,15 +274,15 @@ int live_panels(const Packing& pk) {
 
 // Small-shape path, restarts that the one-workgroup solo kernels take (nmfc_mu_solo_fits(m, n, k): rank <= 8 on
 // gct-sized shapes): each gets 4 (kernel rank <= 4) or 8 stacked columns of its own after the k_small_mu blocks
-// (cols from col_base), in order of kernel rank (one launch per rank), then rank descending, then restart id.
-// Returns the solo jobs; pk grows to hold them.
+// (cols from col_base), highest kernel rank first, then rank descending, then restart id: the order the fused
+// launch starts them in (costliest first).  Returns the solo jobs; pk grows to hold them.
 std::vector<SoloJob> place_solo(Packing& pk, std::vector<RestartInfo> solo, int col_base, int n) {
-  // within a kernel rank the higher ranks first (k_solo8_mu takes k = 5..8 at one cost per iteration, and higher
-  // ranks run longer on average: the dispatcher, which starts a launch's workgroups in order, then starts the likely
-  // stragglers first -- C2's 1 482-iteration k = 8 restart no longer waits for a free CU)
+  // costliest kernel rank first, and within it the higher ranks (k_solo8_mu takes k = 5..8 at one cost per
+  // iteration, and higher ranks run longer on average): the dispatcher, which starts the workgroups in order, then
+  // starts the likely stragglers first
   std::stable_sort(solo.begin(), solo.end(), [n](const RestartInfo& a, const RestartInfo& b) {
     const int ka = nmfc_solo_batch_rank(n, a.k), kb = nmfc_solo_batch_rank(n, b.k);
-    return ka != kb ? ka < kb : a.k != b.k ? a.k > b.k : a.rid < b.rid;
+    return ka != kb ? ka > kb : a.k != b.k ? a.k > b.k : a.rid < b.rid;
   });
   std::vector<SoloJob> jobs;
   int col = col_base;
@@ -1007,46 +1007,51 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       if (!solo.empty() && !team) HCHECK(hipEventRecord(e->fork_ev, st));
       if (!sblocks.empty() && launch_small(e, (int)sblocks.size(), opts.maxiter, opts.stop_rule)) return -1;
       if (!solo.empty()) {
-        // beside k_small_mu on streams of their own (one launch per kernel rank), after it when teams run (a team's
-        // workgroups must all be resident at once: nothing else may hold CUs then).
-        // Beside the block kernel: at most the CUs k_small_mu leaves free (one workgroup of either kernel fills a
-        // CU), shared by the solo launches in proportion to their jobs weighted by the kernels' cost per iteration
-        // (tools/solo_iter_time.py: rank 2 ~3.7 us, 3..4 ~5.7, 5..8 ~12.2), so the block kernel's workgroups never
-        // wait for a CU behind solo workgroups, and each solo workgroup runs its share of jobs one after another
-        // (the budget assumes this engine is the only one on the device: restart groups -- several engines on one
-        // GPU, distributed.RestartGroups -- are a large-shape tool and would oversubscribe it here; a speed matter
-        // only, the bits do not depend on it).  Without blocks (every job a solo job): one workgroup per job, the
-        // launches issued from the highest kernel rank down, so the dispatcher starts the costliest jobs first and
-        // fills the CUs that free up with the rest, across the launches.
+        // after k_small_mu when teams run (a team's workgroups must all be resident at once: nothing else may hold CUs
+        // then), else beside it on streams of their own, one launch per kernel rank, taking at most the CUs it leaves
+        // free (one workgroup of either kernel fills a CU), shared in proportion to jobs x cost per iteration
+        // (tools/solo_iter_time.py: rank 2 ~3.7 us, 3..4 ~5.1, 5..8 ~10.1), each workgroup running its share of jobs
+        // one after another: the block kernel's workgroups never wait for a CU behind solo workgroups (the budget
+        // assumes this engine is the only one on the device; restart groups -- several engines on one GPU -- are a
+        // large-shape tool and would oversubscribe it here; a speed matter only, the bits do not depend on it)
         const bool alone = sblocks.empty() || team;
-        const long free_cu = team ? e->ncu : std::max<long>(1, e->ncu - (long)sblocks.size());
-        auto wt = [](int kp) -> long { return kp <= 2 ? 4 : kp <= 4 ? 6 : 12; };
-        long wsum = 0;
-        for (const SoloJob& jb : solo) wsum += wt(nmfc_solo_batch_rank(n, jb.k));
-        std::vector<std::pair<size_t, size_t>> groups;   // [g0, g1) of one kernel rank, ascending
-        for (size_t g0 = 0; g0 < solo.size();) {
-          const int kp = nmfc_solo_batch_rank(n, solo[g0].k);
-          size_t g1 = g0;
-          while (g1 < solo.size() && nmfc_solo_batch_rank(n, solo[g1].k) == kp) ++g1;
-          groups.emplace_back(g0, g1);
-          g0 = g1;
-        }
-        for (int q = 0; q < (int)groups.size(); ++q) {
-          const size_t g0 = groups[groups.size() - 1 - q].first, g1 = groups[groups.size() - 1 - q].second;
-          const int kp = nmfc_solo_batch_rank(n, solo[g0].k);
-          const long nq = (long)(g1 - g0);
-          const long share = alone ? nq : std::min<long>(nq, std::max<long>(1, free_cu * nq * wt(kp) / wsum));
-          hipStream_t sq = team ? st : e->aux[q];
-          if (!team) HCHECK(hipStreamWaitEvent(sq, e->fork_ev, 0));
+        if (alone) {
+          // the batch's solo jobs have the GPU to themselves: ONE launch of every kernel rank, one workgroup per job
+          // in list order -- the costliest ranks first -- on the main stream (per-rank launches on streams of their
+          // own were serialised by the hardware queues they shared: C2's rank-2 launch began when the rank-4 one ended)
           if (nmfc_solo_batch_launch(e->Acm.as<double>(), e->m_pad, m, n, e->W[0].as<double>(), e->m_pad,
-                                     e->H[0].as<double>(), e->n_pad, e->solojobs.as<SoloJob>() + g0, (int)nq, kp,
+                                     e->H[0].as<double>(), e->n_pad, e->solojobs.as<SoloJob>(), (int)solo.size(), 0,
                                      opts.maxiter, opts.stop_rule, e->stop_iter.as<int>(), e->stop_reason.as<int>(),
-                                     (int)share, sq))
+                                     (int)solo.size(), st))
             return -1;
-          if (!team) {
-            HCHECK(hipEventRecord(e->join_ev[q], sq));
-            HCHECK(hipStreamWaitEvent(st, e->join_ev[q], 0));
+        } else {
+          const long free_cu = std::max<long>(1, e->ncu - (long)sblocks.size());
+          auto wt = [](int kp) -> long { return kp <= 2 ? 4 : kp <= 4 ? 6 : 12; };
+          long wsum = 0;
+          for (const SoloJob& jb : solo) wsum += wt(nmfc_solo_batch_rank(n, jb.k));
+          std::vector<std::pair<size_t, size_t>> groups;   // [g0, g1) of one kernel rank, highest rank first
+          for (size_t g0 = 0; g0 < solo.size();) {
+            const int kp = nmfc_solo_batch_rank(n, solo[g0].k);
+            size_t g1 = g0;
+            while (g1 < solo.size() && nmfc_solo_batch_rank(n, solo[g1].k) == kp) ++g1;
+            groups.emplace_back(g0, g1);
+            g0 = g1;
           }
+          for (int q = 0; q < (int)groups.size(); ++q) {
+            const size_t g0 = groups[q].first, g1 = groups[q].second;
+            const int kp = nmfc_solo_batch_rank(n, solo[g0].k);
+            const long nq = (long)(g1 - g0);
+            const long share = std::min<long>(nq, std::max<long>(1, free_cu * nq * wt(kp) / wsum));
+            HCHECK(hipStreamWaitEvent(e->aux[q], e->fork_ev, 0));
+            if (nmfc_solo_batch_launch(e->Acm.as<double>(), e->m_pad, m, n, e->W[0].as<double>(), e->m_pad,
+                                       e->H[0].as<double>(), e->n_pad, e->solojobs.as<SoloJob>() + g0, (int)nq, kp,
+                                       opts.maxiter, opts.stop_rule, e->stop_iter.as<int>(), e->stop_reason.as<int>(),
+                                       (int)share, e->aux[q]))
+              return -1;
+            HCHECK(hipEventRecord(e->join_ev[q], e->aux[q]));
+          }
+          // the main stream joins after every launch is enqueued
+          for (int q = 0; q < (int)groups.size(); ++q) HCHECK(hipStreamWaitEvent(st, e->join_ev[q], 0));
         }
       }
     }

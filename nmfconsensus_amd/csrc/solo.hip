@@ -96,14 +96,19 @@ struct SoloLayout {
 
 // JOBS: the batched form's job loop (its registers stay out of the single-restart form, whose gct k = 2 case is at
 // the 256-VGPR edge); both forms run the same arithmetic.
-template <int NCG, int KK, int SKIP = 0, int SBO = 0, int SL = 0, bool JOBS = false>
-__global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restrict__ A, int m, int n,
-                                                         double* __restrict__ W, double* __restrict__ H, int maxiter,
-                                                         int stop_rule, int* __restrict__ state, int kt_arg,
-                                                         long long* __restrict__ prof, SoloLayout lay) {
+template <int NCG, int SL>
+using SoloAl = double[SL > 0 ? SL : 1][NCG][64 * SOLO_W];   // A's gene steps SR.. in LDS, lane-contiguous
+
+// The kernel body; its LDS comes from the caller (the kernel's own __shared__ arrays, or the fused batch kernel's
+// buffer), its jobs are jx0, jx0 + jstep, ... of lay.jobs (JOBS) or the one restart.
+template <int NCG, int KK, int SKIP, int SBO, int SL, bool JOBS, bool ONE = false>
+__device__ __forceinline__ void solo_mu_body(const double* __restrict__ A, int m, int n, double* __restrict__ W,
+                                             double* __restrict__ H, int maxiter, int stop_rule,
+                                             int* __restrict__ state, int kt_arg, long long* __restrict__ prof,
+                                             const SoloLayout& lay, SoloSmem<NCG>& sm, SoloAl<NCG, SL>& Al, int jx0,
+                                             int jstep) {
   // gene steps per F batch: larger means fewer H reads from LDS but more live registers (A holds most of them)
   constexpr int SB = SBO ? SBO : KK == 2 ? 8 : 4;
-  __shared__ SoloSmem<NCG> sm;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, K = l >> 4, bq = (l >> 2) & 3, j = l & 3;
   // KK = 4: H in LDS by sample c with its rows rotated by c (row a at position (a - c) & 3), so lane j (samples
   // c = j mod 4) finds row (j + r) & 3 at position r: the F accumulation is rotated by lane and its quad reduction
@@ -111,7 +116,6 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
   constexpr bool ROT = KK == 4;
   auto hp = [](int c, int a) -> int { return ROT ? ((a - c) & 3) : a; };
   constexpr int SR = SOLO_S - SL;   // gene steps of A in registers
-  __shared__ double Al[SL > 0 ? SL : 1][NCG][64 * SOLO_W];   // steps SR.. of A, lane-contiguous
   double a_[SR > 0 ? SR : 1][NCG], w_[SOLO_S];
   // A[gene(s)][4 cg + j] from registers (s < SR) or LDS; s, cg compile-time after unrolling
   auto av = [&](int s, int cg) -> double { return s < SR ? a_[s < SR ? s : 0][cg] : Al[s < SR ? 0 : s - SR][cg][tid]; };
@@ -129,10 +133,10 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
         Al[s < SR ? 0 : s - SR][cg][tid] = v;
     }
   }
-  // batched: jobs blockIdx.x, blockIdx.x + gridDim.x, ... (the grid may be smaller than the job list, so the solo
-  // launches leave CUs to the kernels beside them); one restart otherwise
+  // batched: jobs jx0, jx0 + jstep, ... (the grid may be smaller than the job list, so the solo launches leave CUs
+  // to the kernels beside them); one restart otherwise
   const int njobs = JOBS ? lay.njobs : 1;
-  for (int jx = JOBS ? (int)blockIdx.x : 0; jx < njobs; jx += JOBS ? (int)gridDim.x : 1) {
+  for (int jx = JOBS ? jx0 : 0; jx < (ONE ? jx0 + 1 : njobs); jx += JOBS ? jstep : 1) {   // ONE: job jx0 only
   double* __restrict__ Wj = W;
   double* __restrict__ Hj = H;
   int kt = kt_arg, rid = -1;
@@ -410,6 +414,17 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restric
   }   // jobs
 }
 
+template <int NCG, int KK, int SKIP = 0, int SBO = 0, int SL = 0, bool JOBS = false>
+__global__ __launch_bounds__(64 * SOLO_W) void k_solo_mu(const double* __restrict__ A, int m, int n,
+                                                         double* __restrict__ W, double* __restrict__ H, int maxiter,
+                                                         int stop_rule, int* __restrict__ state, int kt_arg,
+                                                         long long* __restrict__ prof, SoloLayout lay) {
+  __shared__ SoloSmem<NCG> sm;
+  __shared__ SoloAl<NCG, SL> Al;
+  solo_mu_body<NCG, KK, SKIP, SBO, SL, JOBS>(A, m, n, W, H, maxiter, stop_rule, state, kt_arg, prof, lay, sm, Al,
+                                              (int)blockIdx.x, (int)gridDim.x);
+}
+
 // ---- ranks 5..8: the same one-workgroup design with the factor rows in two groups of four ----
 // Lane layout as k_solo_mu; w_[s][h] = W[gene(s)][4 h + j] (zero past the restart's rank kt).  G = W^T A runs two
 // 4x4x4 MFMA chains per (gene step, column group) -- rows 0..3 and 4..7 -- and W^T W three (rows 0-3 x 0-3,
@@ -450,14 +465,12 @@ __device__ __forceinline__ double bsum4(double v) {
 
 // SKIP != 0 only in tools/solobench.hip (phase costs): bit 0 no G / W^T W MFMAs, 1 no F / E / W rule, 2 no h h^T,
 // 3 no stop check, 4 no wave sums, 5 no H update
-template <int NCG, int SL, bool JOBS, int SKIP = 0, int FMQ = JOBS ? 2 : 4>
-__global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restrict__ A, int m, int n,
-                                                          double* __restrict__ W, double* __restrict__ H, int maxiter,
-                                                          int stop_rule, int* __restrict__ state, int kt_arg,
-                                                          SoloLayout lay) {
+template <int NCG, int SL, bool JOBS, int SKIP, int FMQ, bool ONE = false>
+__device__ __forceinline__ void solo8_mu_body(const double* __restrict__ A, int m, int n, double* __restrict__ W,
+                                              double* __restrict__ H, int maxiter, int stop_rule,
+                                              int* __restrict__ state, int kt_arg, const SoloLayout& lay,
+                                              Solo8Smem<NCG>& sm, SoloAl<NCG, SL>& Al, int jx0, int jstep) {
   constexpr int SR = SOLO_S - SL;       // gene steps of A in registers
-  __shared__ Solo8Smem<NCG> sm;
-  __shared__ double Al[SL > 0 ? SL : 1][NCG][64 * SOLO_W];
   const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, K = l >> 4,
             bq = (l >> 2) & 3, j = l & 3;
   double a_[SR > 0 ? SR : 1][NCG], w_[SOLO_S][2];
@@ -476,7 +489,7 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
     }
   }
   const int njobs = JOBS ? lay.njobs : 1;
-  for (int jx = JOBS ? (int)blockIdx.x : 0; jx < njobs; jx += JOBS ? (int)gridDim.x : 1) {
+  for (int jx = JOBS ? jx0 : 0; jx < (ONE ? jx0 + 1 : njobs); jx += JOBS ? jstep : 1) {   // ONE: job jx0 only
   double* __restrict__ Wj = W;
   double* __restrict__ Hj = H;
   int kt = kt_arg, rid = -1;
@@ -745,6 +758,78 @@ __global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restri
   }   // jobs
 }
 
+template <int NCG, int SL, bool JOBS, int SKIP = 0, int FMQ = JOBS ? 2 : 4>
+__global__ __launch_bounds__(64 * SOLO_W) void k_solo8_mu(const double* __restrict__ A, int m, int n,
+                                                          double* __restrict__ W, double* __restrict__ H, int maxiter,
+                                                          int stop_rule, int* __restrict__ state, int kt_arg,
+                                                          SoloLayout lay) {
+  __shared__ Solo8Smem<NCG> sm;
+  __shared__ SoloAl<NCG, SL> Al;
+  solo8_mu_body<NCG, SL, JOBS, SKIP, FMQ>(A, m, n, W, H, maxiter, stop_rule, state, kt_arg, lay, sm, Al,
+                                           (int)blockIdx.x, (int)gridDim.x);
+}
+
+// A batch's solo jobs of every kernel rank in ONE launch (the per-rank launches on streams of their own were
+// serialised by the hardware queues they shared: C2's rank-2 launch started when the rank-4 one ended).  Each
+// workgroup runs jobs jx = blockIdx.x, + gridDim.x, ...; per job the kernel rank picks the body, whose A, LDS and
+// arithmetic are those of the per-rank kernel (the same bits as the drop-in's nmfc_mu_solo).  LDS: one buffer for
+// the largest body.  A2..A8: the bodies' A steps in LDS at this NCG (0 where a rank does not occur).
+template <int NCG>
+constexpr int solo_sl(int kp) {   // A's gene steps in LDS by (column groups, kernel rank): dispatch()'s table
+  return kp == 8 ? (NCG <= 4 ? 0 : NCG <= 6 ? 1 : NCG <= 8 ? 2 : 3) : kp == 4 ? (NCG <= 6 ? 0 : NCG <= 8 ? 1 : 2) : 0;
+}
+template <int NCG>
+constexpr size_t solo_lds_bytes() {
+  constexpr size_t a = sizeof(SoloSmem<NCG>), b = sizeof(Solo8Smem<NCG>);
+  constexpr size_t s4 = ((a + 15) / 16) * 16 + sizeof(SoloAl<NCG, solo_sl<NCG>(4)>);
+  constexpr size_t s8 = ((b + 15) / 16) * 16 + sizeof(SoloAl<NCG, solo_sl<NCG>(8)>);
+  constexpr size_t s2 = ((a + 15) / 16) * 16 + sizeof(SoloAl<NCG, 0>);
+  return s4 > s8 ? (s4 > s2 ? s4 : s2) : (s8 > s2 ? s8 : s2);
+}
+template <int NCG>
+__global__ __launch_bounds__(64 * SOLO_W) void k_solo_batch(const double* __restrict__ A, int m, int n,
+                                                            double* __restrict__ W, double* __restrict__ H,
+                                                            int maxiter, int stop_rule, SoloLayout lay) {
+  __shared__ double lds[solo_lds_bytes<NCG>() / sizeof(double)];
+  auto run = [&](int jx) __attribute__((always_inline)) {
+    const int k = __builtin_amdgcn_readfirstlane(lay.jobs[jx].k);
+    const int kp = k >= 5 ? 8 : (k == 3 && NCG > 8) ? 4 : k;
+    // (an empty asm with a memory clobber opens every arm: the bodies' identical A loads stay in their arms
+    // instead of being hoisted above the branch, where all arms' A registers would be live at once)
+    if (kp == 8) {
+      asm volatile("" ::: "memory");
+      auto& sm = *reinterpret_cast<Solo8Smem<NCG>*>(lds);
+      auto& Al = *reinterpret_cast<SoloAl<NCG, solo_sl<NCG>(8)>*>(lds + (sizeof(Solo8Smem<NCG>) + 15) / 16 * 2);
+      solo8_mu_body<NCG, solo_sl<NCG>(8), true, 0, 2, true>(A, m, n, W, H, maxiter, stop_rule, nullptr, 0, lay, sm, Al,
+                                                              jx, 1);
+    } else {
+      auto& sm = *reinterpret_cast<SoloSmem<NCG>*>(lds);
+      constexpr size_t off = (sizeof(SoloSmem<NCG>) + 15) / 16 * 2;
+      if (kp == 4) {
+        asm volatile("" ::: "memory");
+        auto& Al = *reinterpret_cast<SoloAl<NCG, solo_sl<NCG>(4)>*>(lds + off);
+        solo_mu_body<NCG, 4, 0, 0, solo_sl<NCG>(4), true, true>(A, m, n, W, H, maxiter, stop_rule, nullptr, 0, nullptr,
+                                                                lay, sm, Al, jx, 1);
+      } else if (kp == 3) {
+        if constexpr (NCG <= 8) {
+          asm volatile("" ::: "memory");
+          auto& Al = *reinterpret_cast<SoloAl<NCG, 0>*>(lds + off);
+          solo_mu_body<NCG, 3, 0, 0, 0, true, true>(A, m, n, W, H, maxiter, stop_rule, nullptr, 0, nullptr, lay, sm, Al,
+                                                    jx, 1);
+        }
+      } else {
+        asm volatile("" ::: "memory");
+        auto& Al = *reinterpret_cast<SoloAl<NCG, 0>*>(lds + off);
+        solo_mu_body<NCG, 2, 0, 0, 0, true, true>(A, m, n, W, H, maxiter, stop_rule, nullptr, 0, nullptr, lay, sm, Al,
+                                                  jx, 1);
+      }
+    }
+  };
+  run((int)blockIdx.x);   // one job per workgroup: the grid is the job list
+}
+
+// one restart (nmfc_mu_solo), or one kernel rank's jobs of a batch on persistent workgroups (beside k_small_mu
+// blocks): the per-rank kernels
 template <int NCG, int SL>
 hipError_t launch8(int grid, const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule, int* st,
                    int kt, const SoloLayout& lay, hipStream_t s) {
@@ -766,6 +851,22 @@ hipError_t launch(int grid, const double* A, int m, int n, double* W, double* H,
   else
     hipLaunchKernelGGL((k_solo_mu<NCG, KK, 0, 0, SL, false>), dim3(grid), dim3(64 * SOLO_W), 0, s, A, m, n, W, H,
                        maxiter, stop_rule, st, kt, nullptr, lay);
+  return hipGetLastError();
+}
+
+// every kernel rank of a batch in one k_solo_batch launch, one workgroup per job
+hipError_t dispatch_batch(const double* A, int m, int n, double* W, double* H, int maxiter, int stop_rule,
+                          const SoloLayout& lay, hipStream_t s) {
+  const int ncg = (n + 3) / 4;
+  const dim3 grid(lay.njobs), block(64 * SOLO_W);
+  if (ncg <= 4)
+    hipLaunchKernelGGL((k_solo_batch<4>), grid, block, 0, s, A, m, n, W, H, maxiter, stop_rule, lay);
+  else if (ncg <= 6)
+    hipLaunchKernelGGL((k_solo_batch<6>), grid, block, 0, s, A, m, n, W, H, maxiter, stop_rule, lay);
+  else if (ncg <= 8)
+    hipLaunchKernelGGL((k_solo_batch<8>), grid, block, 0, s, A, m, n, W, H, maxiter, stop_rule, lay);
+  else
+    hipLaunchKernelGGL((k_solo_batch<10>), grid, block, 0, s, A, m, n, W, H, maxiter, stop_rule, lay);
   return hipGetLastError();
 }
 
@@ -947,10 +1048,13 @@ int mu_solo_call(const double* A, int m, int n, int k, int maxiter, int stop_rul
 }
 }  // namespace
 
-// Batched form (nmfc_engine_run, small shapes): jobs of kernel rank kp (solo_rank(n, k) == kp for every job; the
-// engine groups its solo jobs by kp) on min(njobs, max_wgs) workgroups, each running its jobs one after another,
-// reading the engine's column-major Acm and the stacked W/H at each job's col0, stop state into stop_iter /
-// stop_reason[rid].  Returns 0 or -1 (nmfc_last_error).
+// Batched form (nmfc_engine_run, small shapes), reading the engine's column-major Acm and the stacked W/H at each
+// job's col0, stop state into stop_iter / stop_reason[rid]:
+//   kp == 0: the solo jobs of every kernel rank (solo_rank(n, k)) in ONE k_solo_batch launch, one workgroup per
+//            job in list order (the engine lists the costliest ranks first) -- the batch has the GPU to itself;
+//   kp > 0:  the jobs of kernel rank kp on min(njobs, max_wgs) persistent workgroups running their jobs one after
+//            another (beside k_small_mu blocks, which must not wait for CUs behind solo workgroups).
+// Returns 0 or -1 (nmfc_last_error).
 __attribute__((visibility("hidden"))) int nmfc_solo_batch_rank(int n, int k) { return solo_rank(n, k); }
 
 __attribute__((visibility("hidden"))) int nmfc_solo_batch_launch(const double* Acm, long a_ld, int m, int n, double* W,
@@ -959,12 +1063,16 @@ __attribute__((visibility("hidden"))) int nmfc_solo_batch_launch(const double* A
                                                                  int maxiter, int stop_rule, int* stop_iter,
                                                                  int* stop_reason, int max_wgs, hipStream_t st) {
   if (njobs <= 0) return 0;
-  if (!nmfc_mu_solo_fits(m, n, 2) || kp < 2 || (kp > 4 && kp != 8)) {
+  if (!nmfc_mu_solo_fits(m, n, 2) || kp < 0 || kp == 1 || (kp > 4 && kp != 8)) {
     nmfc_set_error("nmfc_solo_batch_launch: shape outside the solo kernel's range");
     return -1;
   }
   const SoloLayout lay{a_ld, w_ld, 1, h_ld, djobs, stop_iter, stop_reason, njobs};
-  const int grid = std::max(1, std::min(njobs, max_wgs > 0 ? max_wgs : njobs));
-  SCHECK(dispatch(grid, kp, Acm, m, n, W, H, maxiter, stop_rule, nullptr, kp, lay, st));
+  if (kp == 0) {
+    SCHECK(dispatch_batch(Acm, m, n, W, H, maxiter, stop_rule, lay, st));
+  } else {
+    const int grid = std::max(1, std::min(njobs, max_wgs > 0 ? max_wgs : njobs));
+    SCHECK(dispatch(grid, kp, Acm, m, n, W, H, maxiter, stop_rule, nullptr, kp, lay, st));
+  }
   return 0;
 }

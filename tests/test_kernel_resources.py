@@ -17,13 +17,15 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "nmfconsensus_amd", "csrc")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-# spilled VGPRs per k_solo_mu<NC, K, ..., JOBS> instantiation (measured round 5, ROCm 7.2 hipcc); every other
-# solo.hip kernel (k_solo8_mu included) must not spill
+# spilled VGPRs per k_solo_mu<NC, K, ..., JOBS> / k_solo_batch<NC> instantiation (measured round 5, ROCm 7.2 hipcc);
+# every other solo.hip kernel (k_solo8_mu included) must not spill
 SOLO_SPILLS = {
     "k_solo_muILi10ELi2ELi0ELi0ELi0ELb0E": 10,   # k = 2 x 40 samples, single restart (the nmf_mu drop-in)
     "k_solo_muILi10ELi2ELi0ELi0ELi0ELb1E": 24,   # the same, batched job loop (C1 / C2)
     "k_solo_muILi10ELi4ELi0ELi0ELi2ELb1E": 1,    # k = 4 x 40, two gene steps in LDS, batched
     "k_solo_muILi8ELi3ELi0ELi0ELi0ELb1E": 2,     # k = 3 x 32, batched
+    "k_solo_muILi10ELi4ELi0ELi0ELi2ELb1E": 3,    # k = 4 x 40, batched beside k_small_mu blocks
+    "k_solo_batchILi10E": 37,                    # every rank x 40 samples in one launch (the rank-2 body's edge)
 }
 
 
