@@ -22,6 +22,27 @@ namespace {
 // packed index of pair (i < j), 0-based, row-wise upper triangle
 inline long ioffst(long n, long i, long j) { return j + i * n - (i + 1) * (i + 2) / 2; }
 
+// First index t of the minimum of d[0..len) if that minimum is strictly below `best` (which it then becomes), else -1:
+// the scan `if (d[t] < best) { best = d[t]; at = t; }` of R's hclust.f, in two passes (a four-way min, then the first
+// index holding it) so the compiler can keep four independent chains instead of one.
+int first_min(const double* d, int len, double& best) {
+  double m0 = best, m1 = best, m2 = best, m3 = best;
+  int t = 0;
+  for (; t + 4 <= len; t += 4) {
+    m0 = d[t] < m0 ? d[t] : m0;
+    m1 = d[t + 1] < m1 ? d[t + 1] : m1;
+    m2 = d[t + 2] < m2 ? d[t + 2] : m2;
+    m3 = d[t + 3] < m3 ? d[t + 3] : m3;
+  }
+  for (; t < len; ++t) m0 = d[t] < m0 ? d[t] : m0;
+  const double m01 = m1 < m0 ? m1 : m0, m23 = m3 < m2 ? m3 : m2, m = m23 < m01 ? m23 : m01;
+  if (!(m < best)) return -1;
+  best = m;
+  for (t = 0; t < len; ++t)
+    if (d[t] == m) return t;
+  return -1;
+}
+
 void hclust_average(int n, std::vector<double>& diss, std::vector<int>& ia, std::vector<int>& ib,
                     std::vector<double>& crit) {
   const double INF = 1e300;
@@ -32,15 +53,11 @@ void hclust_average(int n, std::vector<double>& diss, std::vector<int>& ia, std:
   ib.assign(n, 0);
   crit.assign(n, 0.0);
   int im = 0, jj = 0, jm = 0;
+  // row i's pairs (i, j > i) are contiguous in the packed triangle
   for (int i = 0; i < n - 1; ++i) {
     double dmin = INF;
-    for (int j = i + 1; j < n; ++j) {
-      const double d = diss[ioffst(n, i, j)];
-      if (dmin > d) {
-        dmin = d;
-        jm = j;
-      }
-    }
+    const int t = first_min(&diss[ioffst(n, i, i + 1)], n - 1 - i, dmin);
+    if (t >= 0) jm = i + 1 + t;
     nn[i] = jm;
     disnn[i] = dmin;
   }
@@ -83,18 +100,15 @@ void hclust_average(int n, std::vector<double>& diss, std::vector<int>& ia, std:
     membr[i2] += membr[j2];
     disnn[i2] = dmin;
     nn[i2] = jj;
+    // cluster j2 is gone: its pairs read INF from now on, so the rescans below need no liveness test (an INF never
+    // beats the INF they start from, as a dead j never entered R's scan)
+    for (int k = 0; k < j2; ++k) diss[ioffst(n, k, j2)] = INF;
+    for (int k = j2 + 1; k < n; ++k) diss[ioffst(n, j2, k)] = INF;
     for (int i = 0; i < n - 1; ++i) {
       if (flag[i] && (nn[i] == i2 || nn[i] == j2)) {
         double dm = INF;
-        for (int j = i + 1; j < n; ++j) {
-          if (flag[j]) {
-            const double d = diss[ioffst(n, i, j)];
-            if (d < dm) {
-              dm = d;
-              jj = j;
-            }
-          }
-        }
+        const int t = first_min(&diss[ioffst(n, i, i + 1)], n - 1 - i, dm);
+        if (t >= 0) jj = i + 1 + t;
         nn[i] = jj;
         disnn[i] = dm;
       }
