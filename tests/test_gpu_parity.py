@@ -462,17 +462,24 @@ def test_block_packed_tail_bit_identical():
         assert np.array_equal(a.W[j], b.W[j]) and np.array_equal(a.H[j], b.H[j]), j
 
 
-@pytest.mark.parametrize("ks,R", [([2, 3, 4, 5], 5), ([4, 2], 3), ([8, 6, 5, 7, 9], 3)])
-def test_solo_batch_bitidentical_to_drop_in(golden, oracle, ks, R):
+@pytest.mark.parametrize("ks,R,shape", [([2, 3, 4, 5], 5, None), ([4, 2], 3, None), ([8, 6, 5, 7, 9], 3, None),
+                                        ([2, 3, 4, 5, 8], 2, (700, 30)), ([3, 7, 2], 2, (129, 13))])
+def test_solo_batch_bitidentical_to_drop_in(golden, oracle, ks, R, shape):
     """A sweep's rank 2..8 restarts run on the solo kernels, one workgroup each (batched launches, one per kernel
     rank, beside k_small_mu, which takes k = 9): every such job's W/H, exit and labels are bit-identical to the same
     job through the single-restart drop-in (nmfc_mu_solo with the job's own generateMatrix(ran) init), so a job's
     bits do not depend on the batch.  The gct has n = 40, so k = 3 runs padded to the 4-row kernel (its zero row
-    never mixes in); ranks 5..8 share one kernel (rows past k zero)."""
+    never mixes in); ranks 5..8 share one kernel (rows past k zero).  A batch whose every job is a solo job runs them
+    all in ONE fused launch (k_solo_batch, one workgroup per job); with k = 9 beside them (a k_small_mu block) the
+    per-rank launches run instead.  The synthetic shapes reach the fused kernel's other column-group forms (n = 30:
+    the rank-3 body; n = 13, m = 129: a ragged short matrix)."""
     import ctypes
     from nmfconsensus_amd import _lib
     from nmfconsensus_amd.nmf import Engine
-    A = np.asfortranarray(golden["A_gct"])   # the C ABI takes column-major A
+    if shape is None:
+        A = np.asfortranarray(golden["A_gct"])   # the C ABI takes column-major A
+    else:
+        A = np.asfortranarray(np.random.default_rng(shape[0] + shape[1]).random(shape) + 0.05)
     m, n = A.shape
     seed = 123
     with Engine(A) as eng:
