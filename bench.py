@@ -32,9 +32,10 @@ HBM_PEAK_GBS = 8000.0
 # in lane-instructions per second that is 39.3 T (each FMA, add, mul or divide step counts one)
 FP64_VALU_PEAK_TOPS = FP64_MFMA_PEAK_TFLOPS / 2
 # Brunet: VALU lane-instructions per matrix element and iteration, per side (H update, W update), as compiled
-# (csrc/brunet.hip, tools ISA listing): k FMAs of VP = W H, the divide q = a / VP (v_rcp_f64 + two Newton steps
-# (4 FMA) + mul + residual FMA + correction FMA = 8), k FMAs accumulating W^T Q or Q H^T
-BRUNET_DIV_OPS = 8
+# (csrc/brunet.hip, tools ISA listing): k FMAs of VP = W H, the divide q = a / VP (v_rcp_f64 + one Newton step
+# (2 FMA) + mul + residual FMA + correction FMA = 6; 8 with the second Newton step of rounds 1-4), k FMAs
+# accumulating W^T Q or Q H^T
+BRUNET_DIV_OPS = 6
 
 
 def brunet_valu_ops_per_element(k: int) -> int:
@@ -785,14 +786,16 @@ def bench_brunet(args, rank, world, local, dev):
                 # what `frac` measures (round 4 changed it from rank-k TFLOP/s vs 78.6 TF, which stays as
                 # rank_k_frac_of_78.6TF): compare lines of the same frac_metric only
                 "frac_metric": "fp64 VALU lane-instructions / 39.3 T (2k + BRUNET_DIV_OPS per quotient, pinned to "
-                               "the ISA by tests/test_kernel_resources.py)", "frac_metric_version": 2,
+                               "the ISA by tests/test_kernel_resources.py)",
+                # version 3 (round 5): one Newton step in the divide, BRUNET_DIV_OPS 8 -> 6 per quotient
+                "frac_metric_version": 3,
                 "kernels": kernels,
                 "rank_k_tflops": kernels[dom]["tflops"], "rank_k_frac_of_78.6TF": kernels[dom]["tflops"] / FP64_MFMA_PEAK_TFLOPS,
                 "sweep_valu_tops": sweep_ops / (elapsed / args.steps) / 1e12,
                 "sweep_tflops": sweep_flop / (elapsed / args.steps) / 1e12,
                 "valu_ops_per_element_iteration": {str(k): brunet_valu_ops_per_element(k) for k in ks},
                 "note": "fp64 VALU issue roofline: per matrix element and iteration 2 x (2k FMA + the compiled divide, "
-                        f"{BRUNET_DIV_OPS} VALU instructions: rcp + 2 Newton steps + mul + residual + correction), peak "
+                        f"{BRUNET_DIV_OPS} VALU instructions: rcp + 1 Newton step + mul + residual + correction), peak "
                         "= 1024 SIMDs x 2.4 GHz x 16 fp64 lanes per cycle = 39.3 T lane-instructions/s (the 78.6 TF "
                         "fp64 vector spec / 2); v_rcp_f64 is counted as one slot and address arithmetic not at all, so "
                         "the fraction is a lower bound on VALU issue use; kernel rates from a serialized 40-iteration "

@@ -94,20 +94,20 @@ struct Buf {
   }
 };
 
-// q = a / p: rcp + two Newton steps + one residual correction (Markstein's final step), i.e. the
+// q = a / p: rcp + one Newton step + one residual correction (Markstein's final step), i.e. the
 // compiler's IEEE sequence without its operand-scaling steps (div_scale / div_fmas / div_fixup), which
-// only matter near the exponent limits.  Here a >= 0 and p is a positive rank-k product of
-// [eps, O(1)]-scaled factors; parity to the IEEE-divide oracle is unchanged (tests/test_gpu_brunet.py),
-// and the kernels issue ~10 % fewer VALU cycles per quotient.  NMFC_BRUNET_IEEEDIV restores '/'.
+// only matter near the exponent limits, and without its second Newton step.  v_rcp_f64 is good to
+// 2^-24.4 on gfx950, so one step leaves the reciprocal at ~2^-48.8 and the residual correction's error
+// at ~2^-100 before its rounding: tools/quot_probe.hip found no pair out of 3.2e9 (a, p over 2^-60..2^10)
+// where this differs from the correctly rounded a / p (the two-step form of rounds 1-4 did neither).
+// Here a >= 0 and p is a positive rank-k product of [eps, O(1)]-scaled factors; parity to the IEEE-divide
+// oracle: tests/test_gpu_brunet.py.  NMFC_BRUNET_IEEEDIV restores '/'.
 __device__ __forceinline__ double quot(double a, double p) {
 #ifdef NMFC_BRUNET_IEEEDIV
   return a / p;
 #else
   double r = __builtin_amdgcn_rcp(p);
-  double e = fma(-p, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-p, r, 1.0);
-  r = fma(r, e, r);
+  r = fma(r, fma(-p, r, 1.0), r);
   const double q = a * r;
   return fma(fma(-p, q, a), r, q);
 #endif
