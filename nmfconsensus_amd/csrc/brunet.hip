@@ -140,10 +140,13 @@ constexpr int spl_of(int K) { return (K == 8 || K == 9) ? 2 : 1; }
 #ifndef NMFC_BR_RG7
 #define NMFC_BR_RG7 2
 #endif
+#ifndef NMFC_BR_RG10
+#define NMFC_BR_RG10 2
+#endif
 constexpr int rg_of(int K) {
   return spl_of(K) == 2 ? (K <= 6 ? 2 : 1)
                         : (K <= 2 ? NMFC_BR_RG2 : K <= 3 ? NMFC_BR_RG3 : K <= 4 ? NMFC_BR_RG4 : K <= 5 ? NMFC_BR_RG5
-                           : K <= 6 ? NMFC_BR_RG6 : K <= 7 ? NMFC_BR_RG7 : K <= 10 ? 2 : 1);
+                           : K <= 6 ? NMFC_BR_RG6 : K <= 7 ? NMFC_BR_RG7 : K <= 10 ? NMFC_BR_RG10 : 1);
 }
 // small batches (B <= NMFC_BR_SMALL_B restarts of one k, e.g. one rank's shard of a strong-scaling
 // run): fewer restarts per workgroup so the batch still spreads over the CUs
@@ -193,9 +196,15 @@ __global__ __launch_bounds__(BT) void k_br_init(const uint32_t* __restrict__ see
 // HBM, fetched with coalesced vector loads one tile ahead into registers and stored into the other
 // half of a double-buffered LDS array; the inner loop reads it back with broadcast LDS reads.
 constexpr int TL = 64;
-// inner-loop unroll per k (measured, tools/brunet_kbench.py: unroll 4 is faster for most k, unroll 2
-// where the unrolled live ranges push the register count past an occupancy step)
-constexpr int br_unroll(int K) { return (K == 5 || K == 7 || K == 10) ? 2 : 4; }
+// inner-loop unroll per k (measured, tools/brunet_kbench.py on the C5 shape: unroll 2 where the unrolled live ranges
+// push the register count past an occupancy step; round 5, with the one-step divide, re-measured against 2 / 4 / 8
+// for every k (profiles/r05/brunet/kbench_unroll_rg.txt): 8 for k = 4, 6 (-2.5 %, -10 % hnum + wupd), 2 for k = 8
+// (-12 %), k = 2, 3, 9 tied)
+#ifndef NMFC_BR_UNROLL
+constexpr int br_unroll(int K) { return (K == 4 || K == 6) ? 8 : (K == 5 || K == 7 || K == 8 || K == 10) ? 2 : 4; }
+#else
+constexpr int br_unroll(int) { return NMFC_BR_UNROLL; }   // experiment builds (tools/build_variant.sh)
+#endif
 
 template <int K, int RG>
 struct OperandTiles {
