@@ -117,7 +117,10 @@ __device__ __forceinline__ double quot(double a, double p) {
 // row; where that (rather than the VALU work) bounds the kernel, each row serves 2 elements.  Measured
 // per k (tools/brunet_kbench.py, profiles/r01f_brunet_spl.txt): a gain for k = 8, 9 only -- elsewhere the
 // doubled register state costs more occupancy than the LDS traffic saves.
-constexpr int spl_of(int K) { return (K == 8 || K == 9) ? 2 : 1; }
+#ifndef NMFC_BR_SPL_MASK
+#define NMFC_BR_SPL_MASK ((1 << 8) | (1 << 9))   // bit k set: SPL = 2 for rank k (experiment builds override)
+#endif
+constexpr int spl_of(int K) { return ((NMFC_BR_SPL_MASK >> K) & 1) ? 2 : 1; }
 // restarts per workgroup: each lane keeps SPL * RG * 4K VGPRs of state (operand rows in, accumulators
 // out); RG shares every A element loaded over RG restarts.  Per-k values measured on the C5 shape
 // (profiles/r01g/brunet_rg/): the best RG is not monotone in k because register-count occupancy
@@ -195,7 +198,10 @@ __global__ __launch_bounds__(BT) void k_br_init(const uint32_t* __restrict__ see
 // restarts of a workgroup: TL consecutive gene (sample) rows of K doubles per restart, contiguous in
 // HBM, fetched with coalesced vector loads one tile ahead into registers and stored into the other
 // half of a double-buffered LDS array; the inner loop reads it back with broadcast LDS reads.
-constexpr int TL = 64;
+#ifndef NMFC_BR_TL
+#define NMFC_BR_TL 64
+#endif
+constexpr int TL = NMFC_BR_TL;
 // inner-loop unroll per k (measured, tools/brunet_kbench.py on the C5 shape: unroll 2 where the unrolled live ranges
 // push the register count past an occupancy step; round 5, with the one-step divide, re-measured against 2 / 4 / 8
 // for every k (profiles/r05/brunet/kbench_unroll_rg.txt): 8 for k = 4, 6 (-2.5 %, -10 % hnum + wupd), 2 for k = 8
