@@ -6,6 +6,8 @@ CPU only, no GPU: the GPU pool runs no sanitizer builds, so the host-side C/C++ 
   threads (the batch must equal the one-matrix call bit for bit).
 * the oracle's C restatements (oracle/nmf_oracle.c, oracle/brunet_oracle.c; test infrastructure, the parity
   anchor) built with ASan + UBSan and loaded in a child interpreter that then re-runs golden cases through it.
+* the drop-in's host C (csrc/compat.hip) built with -Xarch_host -fsanitize=address,undefined and driven by
+  tests/sanitize/compat_driver.c (argument / matrix checks, generateMatrix against the golden init).
 """
 import os
 import shutil
@@ -100,3 +102,44 @@ def test_oracle_asan_ubsan():
                            capture_output=True, text=True, timeout=600, env=env)
         assert r.returncode == 0 and "oracle under sanitizers ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
         assert "runtime error" not in r.stderr, r.stderr[-4000:]
+
+
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+CLANG = "/opt/rocm/llvm/bin/clang"
+LIBDIR = os.path.join(ROOT, "nmfconsensus_amd", "lib")
+
+
+@pytest.mark.skipif(not (os.path.exists(HIPCC) and os.path.exists(CLANG)), reason="hipcc / clang not available")
+@pytest.mark.skipif(not os.path.exists(os.path.join(LIBDIR, "libnmf.so")), reason="libnmf.so not built")
+def test_compat_host_asan_ubsan(golden):
+    """The drop-in's host C (csrc/compat.hip: set_default_opts, checkArguments, checkMatrices, randnumber,
+    generateMatrix) compiled with -Xarch_host -fsanitize=address,undefined, linked ahead of the product libnmf.so (its
+    definitions interpose) with tests/sanitize/compat_driver.c: every predicate answers as the reference's, and
+    generateMatrix(ran) after srand(123) equals the reference's golden init bit for bit.  No GPU entry point runs."""
+    import numpy as np
+    with tempfile.TemporaryDirectory() as td:
+        obj, drv, exe, out = (os.path.join(td, x) for x in ("c.o", "d.o", "compat_drv", "out.bin"))
+        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O1", "-g", "-fPIC", "-std=c++17", "-Xarch_host",
+                            "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-c",
+                            os.path.join(CSRC, "compat.hip"), "-o", obj], capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        r = subprocess.run([CLANG, "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-c",
+                            os.path.join(ROOT, "tests", "sanitize", "compat_driver.c"), "-o", drv],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-fsanitize=address", "-fsanitize=undefined",
+                            "-fno-gpu-sanitize", drv, obj, "-L" + LIBDIR, "-lnmf", "-Wl,-rpath," + LIBDIR, "-o", exe],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        r = subprocess.run([exe, out], capture_output=True, text=True, timeout=300, env=ENV)
+        assert r.returncode == 0 and "compat driver ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+        assert "runtime error" not in r.stderr, r.stderr[-4000:]
+        got = np.fromfile(out, dtype=np.float64)
+    m, n, off = 1000, 40, 0
+    for k in (2, 3, 4, 5):
+        W = got[off:off + m * k].reshape((m, k), order="F")
+        off += m * k
+        H = got[off:off + k * n].reshape((k, n), order="F")
+        off += k * n
+        assert np.array_equal(W, golden[f"init_k{k}_W"]) and np.array_equal(H, golden[f"init_k{k}_H"]), k
+    assert off == got.size
