@@ -9,8 +9,11 @@
  *   3. a sharded run (jobs 10..50) of the same engine with caller-provided W / H init and every result array;
  *   4. the drop-in nmf_mu for k = 2..5 on the 1000 x 40 matrix (solo, team) and k = 1, 17 on 300 x 40 (generic);
  *   5. a Brunet sweep, k = 2..4, R = 4, 400 x 30;
- *   6. nmfc_cophenetic_batch on the consensus of run 2.
+ *   6. nmfc_cophenetic_batch on the consensus of run 2;
+ *   7. two host threads, each with an engine of its own over the same matrix, running job shards concurrently (the
+ *      restart groups of distributed.RestartGroups, from C): their counts sum to the one-engine run's.
  * Output: argv[1]/engine_driver.bin (counts, iterations, W / H digests) -- the two builds must agree bit for bit. */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -190,13 +193,82 @@ static int brunet(void) {
   return 0;
 }
 
+struct group_arg {
+  const double* A;
+  int m, n, begin, end, rc;
+  int32_t* counts;
+};
+
+static void* group_run(void* p) {
+  struct group_arg* g = (struct group_arg*)p;
+  const int ks[] = {2, 3, 4, 5, 6, 7, 8, 9, 10};
+  nmfc_sweep_opts o;
+  nmfc_result r;
+  nmfc_engine* e = nmfc_engine_create(-1, g->A, g->m, g->n, 0);
+  g->rc = 1;
+  if (!e) return NULL;
+  nmfc_default_opts(&o);
+  o.maxiter = 3000;
+  o.job_begin = g->begin;
+  o.job_end = g->end;
+  memset(&r, 0, sizeof r);
+  r.counts = g->counts;
+  g->rc = nmfc_engine_run(e, ks, 9, 8, &o, NULL, NULL, &r);
+  nmfc_engine_destroy(e);
+  return NULL;
+}
+
+static int groups(void) {
+  const int m = 2048, n = 96, nk = 9, R = 8, nj = nk * R;
+  const int ks[] = {2, 3, 4, 5, 6, 7, 8, 9, 10};
+  double* A;
+  int32_t *whole = malloc(sizeof(int32_t) * nk * n * n), *c0 = malloc(sizeof(int32_t) * nk * n * n),
+          *c1 = malloc(sizeof(int32_t) * nk * n * n);
+  struct group_arg g[2];
+  pthread_t th[2];
+  nmfc_sweep_opts o;
+  nmfc_result r;
+  long i;
+  int t;
+  sm_state = 99u;
+  A = planted(m, n, 3);
+  if (!A || !whole || !c0 || !c1) return fail("alloc");
+  nmfc_default_opts(&o);
+  o.maxiter = 3000;
+  memset(&r, 0, sizeof r);
+  r.counts = whole;
+  if (nmfc_sweep(A, m, n, ks, nk, R, &o, &r) != 0) return fail("nmfc_sweep whole");
+  for (t = 0; t < 2; ++t) {
+    g[t].A = A;
+    g[t].m = m;
+    g[t].n = n;
+    g[t].begin = t ? nj / 2 : 0;
+    g[t].end = t ? nj : nj / 2;
+    g[t].counts = t ? c1 : c0;
+    if (pthread_create(&th[t], NULL, group_run, &g[t])) return fail("pthread_create");
+  }
+  for (t = 0; t < 2; ++t) pthread_join(th[t], NULL);
+  if (g[0].rc || g[1].rc) return fail("group run");
+  for (i = 0; i < (long)nk * n * n; ++i)
+    if (c0[i] + c1[i] != whole[i]) {
+      fprintf(stderr, "FAIL groups: counts[%ld] %d + %d != %d\n", i, c0[i], c1[i], whole[i]);
+      return 1;
+    }
+  put(whole, sizeof(int32_t) * nk * n * n);
+  free(A);
+  free(whole);
+  free(c0);
+  free(c1);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   char path[4096];
   if (argc < 2) return 2;
   snprintf(path, sizeof path, "%s/engine_driver.bin", argv[1]);
   out = fopen(path, "wb");
   if (!out) return 2;
-  if (sweep_small() || engine_runs() || dropin() || brunet()) return 1;
+  if (sweep_small() || engine_runs() || dropin() || brunet() || groups()) return 1;
   fclose(out);
   printf("engine driver ok\n");
   return 0;
