@@ -119,17 +119,17 @@ def test_compat_host_asan_ubsan(golden):
     import numpy as np
     with tempfile.TemporaryDirectory() as td:
         obj, drv, exe, out = (os.path.join(td, x) for x in ("c.o", "d.o", "compat_drv", "out.bin"))
-        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O1", "-g", "-fPIC", "-std=c++17", "-Xarch_host",
-                            "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-c",
+        hostsan = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined"]
+        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O1", "-g", "-fPIC", "-std=c++17", *hostsan, "-c",
                             os.path.join(CSRC, "compat.hip"), "-o", obj], capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-3000:]
         r = subprocess.run([CLANG, "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-c",
                             os.path.join(ROOT, "tests", "sanitize", "compat_driver.c"), "-o", drv],
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-3000:]
-        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-fsanitize=address", "-fsanitize=undefined",
-                            "-fno-gpu-sanitize", drv, obj, "-L" + LIBDIR, "-lnmf", "-Wl,-rpath," + LIBDIR, "-o", exe],
-                           capture_output=True, text=True, timeout=300)
+        link = ["-fsanitize=address", "-fsanitize=undefined", "-fno-gpu-sanitize"]
+        r = subprocess.run([HIPCC, "--offload-arch=gfx950", *link, drv, obj, "-L" + LIBDIR, "-lnmf",
+                            "-Wl,-rpath," + LIBDIR, "-o", exe], capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-3000:]
         r = subprocess.run([exe, out], capture_output=True, text=True, timeout=300, env=ENV)
         assert r.returncode == 0 and "compat driver ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
