@@ -327,19 +327,31 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
     }
 }
 
+// The workgroup sum of v[c] in the fixed tree order red[t] += red[t + s], s = BT/2, ..., 1: the strides of 64 and
+// more through LDS, the last six inside wave 0 by lane shuffles (lane t adds lane t + s's value of the previous
+// step, exactly the LDS tree's operands), so 3 barriers instead of 9 and the same bits.
 template <int K>
 __device__ __forceinline__ void tree_sum(double (*red)[BT], double* v) {
+  static_assert(BT == 256, "tree_sum: two LDS steps then one wave");
   const int tid = threadIdx.x;
 #pragma unroll
   for (int c = 0; c < K; ++c) red[c][tid] = v[c];
   __syncthreads();
-  for (int s = BT / 2; s > 0; s >>= 1) {
-    if (tid < s) {
+  if (tid < 128) {
 #pragma unroll
-      for (int c = 0; c < K; ++c) red[c][tid] += red[c][tid + s];
-    }
-    __syncthreads();
+    for (int c = 0; c < K; ++c) red[c][tid] += red[c][tid + 128];
   }
+  __syncthreads();
+  if (tid < 64) {
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      double x = red[c][tid] + red[c][tid + 64];
+#pragma unroll
+      for (int s = 32; s > 0; s >>= 1) x = x + __shfl_down(x, s);
+      if (tid == 0) red[c][0] = x;
+    }
+  }
+  __syncthreads();
 #pragma unroll
   for (int c = 0; c < K; ++c) v[c] = red[c][0];
   __syncthreads();
@@ -360,7 +372,21 @@ __global__ __launch_bounds__(BT) void k_br_hupd(int t, int check, int stopconv, 
 #pragma unroll
   for (int c = 0; c < K; ++c) cs[c] = 0.0;
   const double* Wb = W + (long)b * wstride;
-  for (int i = tid; i < m; i += BT) {
+  // this thread's rows i = tid, tid + BT, ... in order, U rows' loads issued ahead of their adds
+  constexpr int U = K <= 8 ? 4 : 2;
+  int i = tid;
+  for (; i + (U - 1) * BT < m; i += U * BT) {
+    double v[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < K; ++c) v[u][c] = Wb[(long)(i + u * BT) * K + c];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < K; ++c) cs[c] += v[u][c];
+  }
+  for (; i < m; i += BT) {
 #pragma unroll
     for (int c = 0; c < K; ++c) cs[c] += Wb[(long)i * K + c];
   }
@@ -375,8 +401,15 @@ __global__ __launch_bounds__(BT) void k_br_hupd(int t, int check, int stopconv, 
 #pragma unroll
     for (int c = 0; c < K; ++c) {
       const double* gp = Gp + ((long)b * K + c) * n_pad + j;
-      double g = 0.0;
-      for (int ch = 0; ch < nchunks; ++ch) g += gp[(long)ch * gp_cs];
+      double g = 0.0;   // the chunk partials in chunk order, eight chunks' loads in flight
+      for (int ch0 = 0; ch0 < nchunks; ch0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ch0 + u < nchunks ? gp[(long)(ch0 + u) * gp_cs] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (ch0 + u < nchunks) g += v[u];
+      }
       hv[c] = __dadd_rn(__dmul_rn(Hb[(long)j * K + c], g), EPS) / cs[c];
       Hb[(long)j * K + c] = hv[c];
       rs[c] += hv[c];
