@@ -176,6 +176,9 @@ def main():
                          "the N > 1 flow with several ranks on one GPU, together with --device)")
     ap.add_argument("--device", type=int, default=None,
                     help="HIP device of this rank (default LOCAL_RANK); rehearsal only")
+    ap.add_argument("--maps-out", default=None,
+                    help="write /proc/self/maps here once the library and the runtime are loaded (with Python's "
+                         "faulthandler on stderr): a native crash's stack addresses can then be symbolized offline")
     ap.add_argument("--cpu-kind", default="reference", choices=["reference", "port"],
                     help="reference: the reference's own nmf_mu (oracle/_ref, fails loudly when absent); port: the "
                          "oracle's C restatement")
@@ -235,6 +238,7 @@ def main():
     if G > 8:
         raise SystemExit(f"--groups {G}: at most 8 restart groups per GPU")
     groups = RestartGroups(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local, groups=G)
+    dump_maps(args.maps_out)
     counts = torch.zeros((nk, n, n), dtype=torch.int32, device=dev)
     timing = not args.no_timing
     from concurrent.futures import ThreadPoolExecutor
@@ -587,6 +591,15 @@ def shard_range_(njobs, rank, world):
     return shard_range(njobs, rank, world)
 
 
+def dump_maps(path):
+    """The process's load map (for symbolizing a native crash's return addresses against the same libraries)."""
+    if path:
+        import faulthandler
+        faulthandler.enable()
+        with open("/proc/self/maps") as src, open(path, "w") as dst:
+            dst.write(src.read())
+
+
 def metric_name(config, m, n, ks):
     if config in ("C3", "C5"):   # BASELINE.json metric, verbatim
         base = "NMF restarts/sec (k=2..10 sweep, 20k×500 fp64) + fp64-MFMA/HBM roofline %"
@@ -706,6 +719,7 @@ def bench_brunet(args, rank, world, local, dev):
     A_dev = torch.from_numpy(A_host.T.copy()).to(dev)
     torch.cuda.synchronize()
     eng = BrunetEngine(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local)
+    dump_maps(args.maps_out)
     counts = torch.zeros((nk, n, n), dtype=torch.int32, device=dev)
     rb, re = shard_range(R, rank, world)
     timing = not args.no_timing

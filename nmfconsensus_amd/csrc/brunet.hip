@@ -22,17 +22,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
+#include "lane_pool.hpp"
 #include "rmt.hpp"
 #include "../../include/nmfc.h"
 
@@ -85,6 +83,36 @@ struct Buf {
   }
   void release() {
     if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+// Pinned host staging of one lane (the per-check stop-iteration read-back, the live-restart list, the seeds): the
+// small per-iteration copies of four lanes never go through HIP's shared pageable staging path.
+struct PinBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipHostMalloc(&p, need, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      br_err("hipHostMalloc(%zu) failed: %s", need, hipGetErrorString(e));
+      p = nullptr;
+      return -1;
+    }
+    bytes = need;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
     p = nullptr;
     bytes = 0;
   }
@@ -575,6 +603,7 @@ enum { BK_HNUM = 0, BK_HUPD = 1, BK_WUPD = 2 };
 struct BrLane {
   hipStream_t st = nullptr;
   Buf W, H, Gp, RS, memb, nochange, stop_iter, act, seeds, labels;
+  PinBuf h_si, h_act, h_seeds;   // pinned host mirrors of stop_iter, act, seeds
   bool timing = false;
   struct Pending {
     int kid;
@@ -588,6 +617,9 @@ struct BrLane {
   void release() {
     Buf* bufs[] = {&W, &H, &Gp, &RS, &memb, &nochange, &stop_iter, &act, &seeds, &labels};
     for (Buf* b : bufs) b->release();
+    h_si.release();
+    h_act.release();
+    h_seeds.release();
     for (auto v : pool) (void)hipEventDestroy(v);
     pool.clear();
     if (st) (void)hipStreamDestroy(st);
@@ -664,10 +696,11 @@ int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o
   hipStream_t st = L->st;
   const long wstride = (long)m * K, hstride = (long)n * K;
   const long gp_cs = (long)B * K * e->n_pad;
-  std::vector<int> act(B), si(B, 0);
-  for (int b = 0; b < B; ++b) act[b] = b;
+  int* act = L->h_act.as<int>();   // pinned (br_run_k sized them): host list of live restart slots
+  int* si = L->h_si.as<int>();     // pinned read-back of stop_iter
+  for (int b = 0; b < B; ++b) act[b] = b, si[b] = 0;
   int nact = B;
-  BCHECK(hipMemcpyAsync(L->act.p, act.data(), sizeof(int) * B, hipMemcpyHostToDevice, st));
+  BCHECK(hipMemcpyAsync(L->act.p, act, sizeof(int) * B, hipMemcpyHostToDevice, st));
   BCHECK(hipMemsetAsync(L->memb.p, 0, sizeof(int) * (size_t)B * n, st));   // old.membership starts at 0
   BCHECK(hipMemsetAsync(L->nochange.p, 0, sizeof(int) * B, st));
   BCHECK(hipMemsetAsync(L->stop_iter.p, 0, sizeof(int) * B, st));
@@ -697,7 +730,7 @@ int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o
     if (check) {
       // stops happen only on check iterations, after that iteration's W update (NMF.div breaks at the
       // end of the iteration): drop stopped restarts from the launch list
-      BCHECK(hipMemcpyAsync(si.data(), L->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+      BCHECK(hipMemcpyAsync(si, L->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
       BCHECK(hipStreamSynchronize(st));
       if (L->timing) br_drain(L);
       int q = 0;
@@ -705,12 +738,12 @@ int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o
         if (si[act[x]] == 0) act[q++] = act[x];
       if (q != nact) {
         nact = q;
-        if (nact > 0) BCHECK(hipMemcpyAsync(L->act.p, act.data(), sizeof(int) * nact, hipMemcpyHostToDevice, st));
+        if (nact > 0) BCHECK(hipMemcpyAsync(L->act.p, act, sizeof(int) * nact, hipMemcpyHostToDevice, st));
         BCHECK(hipStreamSynchronize(st));
       }
     }
   }
-  BCHECK(hipMemcpyAsync(si.data(), L->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+  BCHECK(hipMemcpyAsync(si, L->stop_iter.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
   BCHECK(hipStreamSynchronize(st));
   if (L->timing) br_drain(L);
   iters.resize(B);
@@ -754,14 +787,15 @@ int br_run_k(nmfc_brunet* e, BrLane* L, const KJob& kj, int B, int R, const nmfc
       L->Gp.ensure(sizeof(double) * (size_t)e->nchunks * B * K * e->n_pad) ||
       L->RS.ensure(sizeof(double) * (size_t)B * K) || L->memb.ensure(sizeof(int) * (size_t)B * n) ||
       L->nochange.ensure(sizeof(int) * B) || L->stop_iter.ensure(sizeof(int) * B) || L->act.ensure(sizeof(int) * B) ||
-      L->seeds.ensure(sizeof(uint32_t) * B) || L->labels.ensure(sizeof(int32_t) * (size_t)B * n))
+      L->seeds.ensure(sizeof(uint32_t) * B) || L->labels.ensure(sizeof(int32_t) * (size_t)B * n) ||
+      L->h_si.ensure(sizeof(int) * B) || L->h_act.ensure(sizeof(int) * B) || L->h_seeds.ensure(sizeof(uint32_t) * B))
     return -1;
   const long wstride = (long)m * K, hstride = (long)n * K;
   std::vector<double> hw, hh;
-  std::vector<uint32_t> seeds(B);
+  uint32_t* seeds = L->h_seeds.as<uint32_t>();
   const int rb = std::max(0, o.restart_begin);
   for (int b = 0; b < B; ++b) seeds[b] = o.seed + (uint32_t)(rb + b + 1);   // set.seed(rseed + i), i 1-based
-  BCHECK(hipMemcpyAsync(L->seeds.p, seeds.data(), sizeof(uint32_t) * B, hipMemcpyHostToDevice, st));
+  BCHECK(hipMemcpyAsync(L->seeds.p, seeds, sizeof(uint32_t) * B, hipMemcpyHostToDevice, st));
   if (W_init && H_init) {
     // caller factors for this k's B jobs: W_b m x K column-major, H_b K x n column-major
     hw.assign((size_t)B * m * K, 0.0);
@@ -955,10 +989,6 @@ int nmfc_brunet_run(nmfc_brunet* e, const int* ks, int nk, int R, const nmfc_bru
   std::vector<KJob> order(jobs);
   std::stable_sort(order.begin(), order.end(), [](const KJob& a, const KJob& b) { return a.K > b.K; });
   const int nl = std::min(o.lanes > 0 ? std::min(o.lanes, BR_LANES) : e->nlanes, nk);
-  std::atomic<int> next{0};
-  std::atomic<int> failed{0};
-  std::string first_err;
-  std::mutex mu;
   std::vector<long long> lane_iters(nl, 0);
   std::vector<int> lane_max(nl, 0);
   for (int l = 0; l < nl; ++l) {
@@ -966,23 +996,16 @@ int nmfc_brunet_run(nmfc_brunet* e, const int* ks, int nk, int R, const nmfc_bru
     L.timing = e->timing;
     for (int q = 0; q < 3; ++q) L.kms[q] = 0, L.kcount[q] = 0, L.kfl_sum[q] = 0;
   }
-  auto worker = [&](int l) {
-    BrLane* L = &e->lanes[l];
-    for (;;) {
-      const int idx = next.fetch_add(1);
-      if (idx >= nk || failed.load()) break;
-      if (br_run_k(e, L, order[idx], B, R, o, W_init, H_init, dcounts, out, &lane_iters[l], &lane_max[l])) {
-        std::lock_guard<std::mutex> g(mu);
-        if (!failed.exchange(1)) first_err = nmfc_last_error();
-        break;
-      }
-    }
-  };
-  std::vector<std::thread> th;
-  for (int l = 1; l < nl; ++l) th.emplace_back(worker, l);
-  worker(0);
-  for (auto& t : th) t.join();
-  if (failed.load()) {
+  // the k batches, largest first, on nl lanes (csrc/lane_pool.hpp; the scheduler alone runs under TSan in the CPU
+  // suite): a lane touches only its own BrLane, its lane_iters / lane_max slot and the outputs of its k
+  std::string first_err;
+  const int rc = nmfc_host::run_lanes(
+      nl, nk,
+      [&](int l, int idx) {
+        return br_run_k(e, &e->lanes[l], order[idx], B, R, o, W_init, H_init, dcounts, out, &lane_iters[l], &lane_max[l]);
+      },
+      [] { return std::string(nmfc_last_error()); }, &first_err);
+  if (rc) {
     nmfc_set_error(first_err.c_str());
     return -1;
   }

@@ -143,3 +143,24 @@ def test_compat_host_asan_ubsan(golden):
         off += k * n
         assert np.array_equal(W, golden[f"init_k{k}_W"]) and np.array_equal(H, golden[f"init_k{k}_H"]), k
     assert off == got.size
+
+
+LANE_DRIVER = os.path.join(ROOT, "tests", "sanitize", "lane_pool_driver.cpp")
+
+
+@pytest.mark.skipif(GXX is None, reason="g++ not available")
+@pytest.mark.parametrize("san", ["thread", "address,undefined"])
+def test_brunet_lane_pool_sanitized(san):
+    """The Brunet sweep's lane scheduler (csrc/lane_pool.hpp: 4 host threads, one per HIP stream, taking k batches
+    from one atomic counter; brunet.hip nmfc_brunet_run) with a stub job that grows per-lane scratch, sets the
+    thread-local error string and writes its own output slot: under ThreadSanitizer and under ASan + UBSan, 1..8
+    lanes, every job exactly once, outputs equal to a serial run, a failure reported with its own message."""
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "lane_pool_driver")
+        extra = ["-fno-sanitize-recover=all"] if "undefined" in san else []
+        r = subprocess.run([GXX, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={san}", *extra,
+                            "-pthread", LANE_DRIVER, "-o", exe], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=ENV)
+        assert r.returncode == 0 and "lane pool driver ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+        assert "WARNING: ThreadSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
