@@ -359,19 +359,10 @@ def main():
             roof["note"] += (f"; {G} restart groups per GPU on their own streams: a kernel's HIP-event duration "
                              "includes the other groups' concurrent kernels, so these per-kernel rates are lower "
                              "bounds (the N = 1 line, 1 group, is the per-kernel measurement)")
-        tp = pmc_profile_for(args.config)
+        tp = pmc_profile_for({"config": args.config, "stop_rule": args.stop_rule, "maxiter": args.maxiter,
+                              "restarts": R})
         if tp:
-            per, src = tp
-            note = (f"HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, {src}, same kernel source), "
-                    "averaged over every launch of one C3 sweep like `achieved`")
-            if dom in per:
-                roof["traffic"], roof["traffic_unit"] = per[dom], note
-            for kname, b in per.items():
-                if kname in kernels:
-                    kr = kernels[kname]
-                    kr["traffic_bytes_per_launch"] = b
-                    kr["traffic_gbs"] = b / (kr["avg_ms"] * 1e-3) / 1e9
-                    kr["traffic_frac_hbm"] = kr["traffic_gbs"] / HBM_PEAK_GBS
+            attach_traffic(roof, kernels, dom, *tp)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -525,8 +516,8 @@ def bench_simulated_world(args, dev):
 
     W = args.simulate_world
     m, n, ks, R, _ = CONFIGS[args.config]
-    if args.config == "C4":
-        R = R // 8
+    # C4 is replayed as the whole 8-GPU job of BASELINE configs[3] (R = 1000 over W shards, 1750 jobs each at W = 8),
+    # not the per-GPU share the C4 line runs
     if args.restarts:
         R = args.restarts
     nk = len(ks)
@@ -546,7 +537,10 @@ def bench_simulated_world(args, dev):
         _, res = run_sharded_sweep(grp, ks, R, rank=r, world=W, counts_tensor=part, reduce=False,
                                    maxiter=args.maxiter, seed=123, stop_rule=stop_rule, check_every=args.check_every)
         torch.cuda.synchronize()
-        return time.perf_counter() - t0, res
+        dt = time.perf_counter() - t0
+        log(f"[sim{W}] shard {r}: {len(res.iters)} jobs, {dt:.3f} s, mean iters {np.mean(res.iters):.1f}, "
+            f"max {int(np.max(res.iters))}")
+        return dt, res
 
     for _ in range(args.warmup):
         for r in range(W):
@@ -554,21 +548,36 @@ def bench_simulated_world(args, dev):
     for s_ in range(args.steps):
         total.zero_()
         its = []
+        shard_maxit = []
         for r in range(W):
             shard_s[s_, r], res = shard(r)
             total += part
             its.append(res.iters)
+            shard_maxit.append(int(np.max(res.iters)))
         iters = np.concatenate(its)
     grp.close()
     worst = shard_s.max(axis=1).mean()
     value = nk * R / worst
-    # the sum of the shards' counts equals one whole sweep's (placement never changes a bit)
-    ref = RestartGroups(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=dev.index, groups=1)
-    whole = torch.zeros_like(part)
-    _, rw = run_sharded_sweep(ref, ks, R, rank=0, world=1, counts_tensor=whole, reduce=False, maxiter=args.maxiter,
-                              seed=123, stop_rule=stop_rule, check_every=args.check_every)
-    ref.close()
-    same = bool(torch.equal(whole, total)) and bool(np.array_equal(rw.iters, iters))
+    if args.dump_iters:
+        np.save(args.dump_iters, np.stack([np.asarray(ks)[np.arange(nk * R) % nk], iters]))
+    import hashlib
+    counts_host = total.cpu().numpy()
+    counts_sha = hashlib.sha256(counts_host.tobytes()).hexdigest()
+    diag_ok = bool(all(np.all(np.diagonal(counts_host[i]) == R) for i in range(nk)))
+    sym_ok = bool(np.array_equal(counts_host, np.transpose(counts_host, (0, 2, 1))))
+    if nk * R <= 4000:
+        # the sum of the shards' counts equals one whole sweep's (placement never changes a bit)
+        ref = RestartGroups(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=dev.index, groups=1)
+        whole = torch.zeros_like(part)
+        _, rw = run_sharded_sweep(ref, ks, R, rank=0, world=1, counts_tensor=whole, reduce=False, maxiter=args.maxiter,
+                                  seed=123, stop_rule=stop_rule, check_every=args.check_every)
+        ref.close()
+        same = bool(torch.equal(whole, total)) and bool(np.array_equal(rw.iters, iters))
+    else:
+        # the whole job on one GPU would take as long as all shards again (C4: 14 000 jobs); the shards' summed
+        # counts are checked for the invariants instead (diagonal = R, symmetric) and fingerprinted, and
+        # --dump-iters lets the golden jobs of every shard be compared with the reference offline
+        same = None
     out = {
         "metric": metric_name(args.config, m, n, ks) + f" [one-GPU replay of the {W}-GPU strong-scaling shards]",
         "value": value, "unit": "restarts/s", "n_gpus": 1, "simulated_world": W, "steps": args.steps,
@@ -578,11 +587,13 @@ def bench_simulated_world(args, dev):
                                f"{nk * R} jobs split into {W} shard_range slices, {G} restart groups each",
                    "per_gpu_restarts_per_s": value / W, "shard_seconds": shard_s.mean(axis=0).tolist(),
                    "shard_jobs": [int(b - a) for a, b in (shard_range_(nk * R, r, W) for r in range(W))],
-                   "counts_equal_whole_sweep": same, "mean_iterations": float(iters.mean()),
+                   "counts_equal_whole_sweep": same, "counts_sum_sha256": counts_sha,
+                   "counts_diag_equals_R": diag_ok, "counts_symmetric": sym_ok,
+                   "shard_max_iterations": [int(x) for x in shard_maxit], "mean_iterations": float(iters.mean()),
                    "max_iterations": int(iters.max())},
     }
     print(json.dumps(out), flush=True)
-    if not same:
+    if same is False or not (diag_ok and sym_ok):
         raise SystemExit("simulated shards' counts differ from the whole sweep")
 
 
@@ -666,15 +677,20 @@ PMC_NAMES = {"wta": ("k_wta2", "k_wta_narrow", "k_wta_narrow_lc"), "ahtw": ("k_a
              "labels": ("k_labels",), "counts": ("k_counts",)}
 
 
-def pmc_profile_for(config):
+# the workload tools/profile_round.sh profiles (the default C3 line); profiles written before round 6 carry no
+# "workload" record and were all taken on exactly this command
+PMC_DEFAULT_WORKLOAD = {"config": "C3", "stop_rule": "ref_compat", "maxiter": 10000, "restarts": 200}
+
+
+def pmc_profile_for(workload):
     """HBM bytes per launch of the engine kernels from the newest committed PMC passes (tools/profile_round.sh:
-    FETCH_SIZE x 2 + WRITE_SIZE, averaged over every launch of one C3 sweep like `achieved`; the variants of one
+    FETCH_SIZE x 2 + WRITE_SIZE, averaged over every launch of one sweep like `achieved`; the variants of one
     kernel pooled by launch count) -- used only when the profile was taken on THIS kernel source (its recorded
-    source hash matches), so the figures cannot go stale silently.  Returns ({kernel: bytes}, source) or None."""
+    source hash matches) AND on this line's workload (config, stop rule, maxiter, restarts: a FIXED-1000 sweep
+    launches every kernel at full load, so a REF_COMPAT sweep's per-launch average does not describe it), so the
+    figures cannot go stale or be borrowed silently.  Returns ({kernel: bytes}, source) or None."""
     from nmfconsensus_amd.build import source_sha256
 
-    if config != "C3":
-        return None
     import glob
     sha = source_sha256()
     for tp in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_traffic.json"), recursive=True), reverse=True):
@@ -682,7 +698,7 @@ def pmc_profile_for(config):
             pm = json.load(open(tp))
         except Exception:
             continue
-        if pm.get("source_sha256") != sha:
+        if pm.get("source_sha256") != sha or pm.get("workload", PMC_DEFAULT_WORKLOAD) != workload:
             continue
         per = {}
         for k, names in PMC_NAMES.items():
@@ -690,8 +706,32 @@ def pmc_profile_for(config):
             if rows:
                 per[k] = sum(r["hbm_bytes_per_launch"] * r["launches"] for r in rows) / sum(r["launches"] for r in rows)
         return per, os.path.relpath(tp, ROOT)
-    log("[bench] no committed PMC profile matches this kernel source: roofline.traffic = null")
+    log(f"[bench] no committed PMC profile matches this kernel source and workload {workload}: roofline.traffic = null")
     return None
+
+
+def attach_traffic(roof, kernels, dom, per, src):
+    """Counter bytes per launch into the roofline object.  Counter traffic can never be below the algorithmic bytes
+    (every algorithmic byte crosses HBM at least once): a profile that says so describes another workload, and
+    its figure is dropped (null, with the reason) instead of reported."""
+    note = (f"HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, {src}, same kernel source and workload), "
+            "averaged over every launch of one sweep like `achieved`")
+    rejected = []
+    for kname, b in per.items():
+        if kname not in kernels:
+            continue
+        kr = kernels[kname]
+        if b < kr.get("algo_bytes_per_launch", 0.0):
+            rejected.append(kname)
+            continue
+        kr["traffic_bytes_per_launch"] = b
+        kr["traffic_gbs"] = b / (kr["avg_ms"] * 1e-3) / 1e9
+        kr["traffic_frac_hbm"] = kr["traffic_gbs"] / HBM_PEAK_GBS
+    if dom in per and dom not in rejected:
+        roof["traffic"], roof["traffic_unit"] = per[dom], note
+    if rejected:
+        roof["traffic_rejected"] = (f"{src}: counter bytes below the algorithmic bytes for {rejected} -- not this "
+                                    "workload's traffic; reported as null")
 
 
 def bench_brunet(args, rank, world, local, dev):

@@ -6,7 +6,11 @@ doubled; WRITE_SIZE is taken as is.
 
 Two averages per kernel: over ALL launches of the profiled sweep (what bench.py's roofline `achieved`
 is averaged over: every launch of one REF_COMPAT sweep) and over the full-load launches (the first
-100: every restart is still running before iteration 400).  Prints JSON."""
+100: every restart is still running before iteration 400).  Prints JSON.
+
+  tools/pmc_traffic.py <profile dir> [config stop_rule maxiter restarts]
+The workload the passes profiled (default: the C3 bench line's, C3 ref_compat 10000 200) is recorded in the JSON;
+bench.py attaches the figures only to a line of the same workload (config, stop rule, maxiter, restarts)."""
 import collections
 import csv
 import glob
@@ -40,4 +44,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nmfconsensus_amd.build import source_sha256  # noqa: E402
 
 out["source_sha256"] = source_sha256()   # bench.py uses this profile only for the same kernel source
+wl = sys.argv[2:6] if len(sys.argv) >= 6 else ["C3", "ref_compat", "10000", "200"]
+out["workload"] = {"config": wl[0], "stop_rule": wl[1], "maxiter": int(wl[2]), "restarts": int(wl[3])}
 print(json.dumps(out, indent=1))
