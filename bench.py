@@ -36,6 +36,8 @@ FP64_VALU_PEAK_TOPS = FP64_MFMA_PEAK_TFLOPS / 2
 # (2 FMA) + mul + residual FMA + correction FMA = 6; 8 with the second Newton step of rounds 1-4), k FMAs
 # accumulating W^T Q or Q H^T
 BRUNET_DIV_OPS = 6
+# restart groups for the whole job on one GPU (the default C3 line): the fastest measured policy
+N1_GROUPS = 2
 
 
 def brunet_valu_ops_per_element(k: int) -> int:
@@ -151,8 +153,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check-every", type=int, default=4, help="MU iterations enqueued between stop polls")
     ap.add_argument("--groups", type=int, default=0,
-                    help="restart groups per GPU (engines on their own streams); 0 = auto: 2 for a strong-scaling "
-                         "shard (N > 1), else 1")
+                    help="restart groups per GPU (engines on their own streams); 0 = auto: N1_GROUPS for the whole "
+                         "job on one GPU, 2 for a strong-scaling shard (N > 1)")
+    ap.add_argument("--roofline-steps", type=int, default=1,
+                    help="sweeps of the separate one-group roofline pass when the timed steps use G > 1 groups")
     ap.add_argument("--overlap-host", action="store_true",
                     help="run each sweep's cophenetic step on a host thread beside the next sweep's GPU work")
     ap.add_argument("--cpu-iters", type=int, default=100, help="iterations per k in the CPU sample (~20 s wall on 16 cores)")
@@ -230,11 +234,17 @@ def main():
     A_dev = torch.from_numpy(A_host.T.copy()).to(dev)          # (n, m) row-major == (m, n) column-major
     torch.cuda.synchronize()
     # G restart groups per GPU (distributed.RestartGroups: G engines on their own HIP streams over the same A,
-    # driven from G host threads, counts summed on the device; +1 to +2.4 % at R = 25..200 per GPU, DESIGN.md
-    # section 5).  Auto: 2 groups for a strong-scaling shard (N > 1), 1 for the whole job on one GPU, whose line
-    # is the per-kernel roofline measurement (overlapping groups stretch every kernel's HIP-event duration).
+    # driven from G host threads, counts summed on the device).  Auto: the fastest measured
+    # policy -- N1_GROUPS for the whole job on one GPU, 2 for a strong-scaling shard (N > 1).  Overlapping groups
+    # stretch every kernel's HIP-event duration, so with G > 1 the per-kernel roofline comes from a separate
+    # one-group timed pass over the same shard after the timed steps (outside the timed region).
     jb, je = shard_range(nk * R, rank, world)
-    G = args.groups if args.groups > 0 else (2 if (world > 1 and args.scaling == "strong" and je - jb >= 2) else 1)
+    if args.groups > 0:
+        G = args.groups
+    elif world > 1:
+        G = 2 if (args.scaling == "strong" and je - jb >= 2) else 1
+    else:
+        G = N1_GROUPS if je - jb >= N1_GROUPS else 1
     if G > 8:
         raise SystemExit(f"--groups {G}: at most 8 restart groups per GPU")
     groups = RestartGroups(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local, groups=G)
@@ -271,7 +281,8 @@ def main():
     if pending[0] is not None:
         pending[0].result()
         pending[0] = None
-    groups.set_timing(timing, args.timing_stride)
+    roof_pass = timing and G > 1   # per-kernel rates from a separate one-group pass (below)
+    groups.set_timing(timing and not roof_pass, args.timing_stride)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -299,6 +310,24 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    if roof_pass:
+        # the roofline pass: this rank's same shard on ONE restart group, HIP events as in a one-group line, after the
+        # timed region (its time is not in `value`); its iterations must equal the timed sweeps' (placement never
+        # changes a bit)
+        one = RestartGroups(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=local, groups=1)
+        scratch = torch.zeros_like(counts)
+        one.set_timing(True, args.timing_stride)
+        for _ in range(args.roofline_steps):
+            _, r1 = run_sharded_sweep(one, ks, R, rank=rank, world=world, counts_tensor=scratch, reduce=False,
+                                      maxiter=args.maxiter, seed=123, stop_rule=stop_rule, check_every=args.check_every)
+            for kid, a in acc.items():
+                for i, v in enumerate(one.kernel_stats(kid)):
+                    a[i] += v
+            if not np.array_equal(r1.iters, last[0].iters):
+                raise SystemExit("roofline pass: iterations differ from the timed sweeps")
+        one.close()
+        torch.cuda.synchronize()
 
     res, rho = last
     if args.dump_iters and rank == 0:
@@ -355,10 +384,12 @@ def main():
                          "launch; 'launches' counts the timed ones); kernels[*] with bound 'hbm': algorithmic bytes "
                          "per launch / mean duration vs 8 TB/s"),
                 "timing_stride": args.timing_stride}
-        if G > 1:
-            roof["note"] += (f"; {G} restart groups per GPU on their own streams: a kernel's HIP-event duration "
-                             "includes the other groups' concurrent kernels, so these per-kernel rates are lower "
-                             "bounds (the N = 1 line, 1 group, is the per-kernel measurement)")
+        if roof_pass:
+            roof["note"] += (f"; the timed steps ran {G} restart groups per GPU on their own streams (whose "
+                             "concurrent kernels would stretch each other's HIP-event durations), so these per-kernel "
+                             f"rates come from a separate one-group pass over the same shard ({args.roofline_steps} "
+                             "sweep(s), after the timed region, iterations checked equal)")
+            roof["source"] = f"one-group roofline pass, {args.roofline_steps} sweep(s)"
         tp = pmc_profile_for({"config": args.config, "stop_rule": args.stop_rule, "maxiter": args.maxiter,
                               "restarts": R})
         if tp:

@@ -196,6 +196,12 @@ void nmfc_nmf_mu_release(void);
 
 /* Diagnostics. */
 const char* nmfc_last_error(void);
+
+/* The compile-time tuning switches this library was built with, "NAME=value;..." as the preprocessor saw them in the
+ * MU engine's / the Brunet kernels' translation unit (csrc/nmfc_tuning.hpp lists each with its product default; the
+ * CPU suite checks the product build against those defaults). */
+const char* nmfc_build_tuning(void);
+const char* nmfc_build_tuning_brunet(void);
 const char* nmfc_version(void);
 /* Per-kernel device time (ms) accumulated over the last run, measured with HIP events on the
  * engine's stream: kernel ids 0 = wta (W^T A + W^T W, MFMA), 1 = hupdate (H update + stop check),

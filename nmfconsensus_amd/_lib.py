@@ -61,7 +61,7 @@ EXPORTED = [
     "nmfc_engine_set_timing", "nmfc_engine_kernel_flops", "nmfc_engine_kernel_bytes",
     "nmfc_calculate_norm_dev", "nmfc_calculate_maxchange_dev", "nmfc_nmf_mu_release",
     "nmfc_brunet_default_opts", "nmfc_brunet_create", "nmfc_brunet_destroy", "nmfc_brunet_run",
-    "nmfc_brunet_set_timing", "nmfc_brunet_kernel_time",
+    "nmfc_brunet_set_timing", "nmfc_brunet_kernel_time", "nmfc_build_tuning", "nmfc_build_tuning_brunet",
 ]
 
 _LIB = None

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib", "libnmf.so")
 SOURCES = ["engine.hip", "compat.hip", "brunet.hip", "generic.hip", "solo.hip", "hclust.cpp"]
-HEADERS = ["nmfc_kernels.hpp", "rmt.hpp", "../../include/nmfc.h", "../../include/libnmf_compat.h"]
+HEADERS = ["nmfc_kernels.hpp", "nmfc_tuning.hpp", "lane_pool.hpp", "rmt.hpp", "../../include/nmfc.h", "../../include/libnmf_compat.h"]
 ARCH = os.environ.get("NMFC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -23,7 +23,7 @@ def source_sha256() -> str:
     """Hash of the engine's kernel + host sources: tags PMC profiles with the code they measured."""
     import hashlib
     h = hashlib.sha256()
-    for f in ("nmfc_kernels.hpp", "engine.hip"):
+    for f in ("nmfc_kernels.hpp", "engine.hip", "nmfc_tuning.hpp"):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()

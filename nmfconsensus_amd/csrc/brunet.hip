@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "lane_pool.hpp"
+#include "nmfc_tuning.hpp"
 #include "rmt.hpp"
 #include "../../include/nmfc.h"
 
@@ -126,12 +127,15 @@ struct PinBuf {
 // compiler's IEEE sequence without its operand-scaling steps (div_scale / div_fmas / div_fixup), which
 // only matter near the exponent limits, and without its second Newton step.  v_rcp_f64 is good to
 // 2^-24.4 on gfx950, so one step leaves the reciprocal at ~2^-48.8 and the residual correction's error
-// at ~2^-100 before its rounding: tools/quot_probe.hip found no pair out of 3.2e9 (a, p over 2^-60..2^10)
-// where this differs from the correctly rounded a / p (the two-step form of rounds 1-4 did neither).
-// Here a >= 0 and p is a positive rank-k product of [eps, O(1)]-scaled factors; parity to the IEEE-divide
-// oracle: tests/test_gpu_brunet.py.  NMFC_BRUNET_IEEEDIV restores '/'.
+// at ~2^-97 relative before its rounding: the result is FAITHFUL, and it matched the correctly rounded a / p
+// on every one of 3.2e9 random probe pairs (tools/quot_probe.hip, a, p over 2^-60..2^10) -- but it is not
+// proven correctly rounded: a quotient can sit closer to a rounding midpoint (down to ~2^-106) than the
+// remaining error, and random pairs almost never hit those cases, so bit parity with an IEEE divide is
+// unpinned for them.  Here a >= 0 and p is a positive rank-k product of [eps, O(1)]-scaled factors; parity to
+// the IEEE-divide oracle on the tested sweeps: tests/test_gpu_brunet.py.  NMFC_BRUNET_IEEEDIV (a build of
+// tools/build_variant.sh) is the exact IEEE option.
 __device__ __forceinline__ double quot(double a, double p) {
-#ifdef NMFC_BRUNET_IEEEDIV
+#if NMFC_BRUNET_IEEEDIV
   return a / p;
 #else
   double r = __builtin_amdgcn_rcp(p);
@@ -145,35 +149,11 @@ __device__ __forceinline__ double quot(double a, double p) {
 // row; where that (rather than the VALU work) bounds the kernel, each row serves 2 elements.  Measured
 // per k (tools/brunet_kbench.py, profiles/r01f_brunet_spl.txt): a gain for k = 8, 9 only -- elsewhere the
 // doubled register state costs more occupancy than the LDS traffic saves.
-#ifndef NMFC_BR_SPL_MASK
-#define NMFC_BR_SPL_MASK ((1 << 8) | (1 << 9))   // bit k set: SPL = 2 for rank k (experiment builds override)
-#endif
 constexpr int spl_of(int K) { return ((NMFC_BR_SPL_MASK >> K) & 1) ? 2 : 1; }
 // restarts per workgroup: each lane keeps SPL * RG * 4K VGPRs of state (operand rows in, accumulators
 // out); RG shares every A element loaded over RG restarts.  Per-k values measured on the C5 shape
 // (profiles/r01g/brunet_rg/): the best RG is not monotone in k because register-count occupancy
 // steps and grid size (groups = R / RG) move together; RG never changes a restart's arithmetic.
-#ifndef NMFC_BR_RG2
-#define NMFC_BR_RG2 5
-#endif
-#ifndef NMFC_BR_RG3
-#define NMFC_BR_RG3 4
-#endif
-#ifndef NMFC_BR_RG4
-#define NMFC_BR_RG4 5
-#endif
-#ifndef NMFC_BR_RG5
-#define NMFC_BR_RG5 4
-#endif
-#ifndef NMFC_BR_RG6
-#define NMFC_BR_RG6 2
-#endif
-#ifndef NMFC_BR_RG7
-#define NMFC_BR_RG7 2
-#endif
-#ifndef NMFC_BR_RG10
-#define NMFC_BR_RG10 2
-#endif
 constexpr int rg_of(int K) {
   return spl_of(K) == 2 ? (K <= 6 ? 2 : 1)
                         : (K <= 2 ? NMFC_BR_RG2 : K <= 3 ? NMFC_BR_RG3 : K <= 4 ? NMFC_BR_RG4 : K <= 5 ? NMFC_BR_RG5
@@ -181,12 +161,6 @@ constexpr int rg_of(int K) {
 }
 // small batches (B <= NMFC_BR_SMALL_B restarts of one k, e.g. one rank's shard of a strong-scaling
 // run): fewer restarts per workgroup so the batch still spreads over the CUs
-#ifndef NMFC_BR_SMALL_B
-#define NMFC_BR_SMALL_B 32
-#endif
-#ifndef NMFC_BR_RG_SMALL_DIV
-#define NMFC_BR_RG_SMALL_DIV 0
-#endif
 constexpr int rg_small(int K) {
   return NMFC_BR_RG_SMALL_DIV == 0 ? 1 : (rg_of(K) / NMFC_BR_RG_SMALL_DIV > 1 ? rg_of(K) / NMFC_BR_RG_SMALL_DIV : 1);
 }
@@ -226,19 +200,15 @@ __global__ __launch_bounds__(BT) void k_br_init(const uint32_t* __restrict__ see
 // restarts of a workgroup: TL consecutive gene (sample) rows of K doubles per restart, contiguous in
 // HBM, fetched with coalesced vector loads one tile ahead into registers and stored into the other
 // half of a double-buffered LDS array; the inner loop reads it back with broadcast LDS reads.
-#ifndef NMFC_BR_TL
-#define NMFC_BR_TL 64
-#endif
 constexpr int TL = NMFC_BR_TL;
 // inner-loop unroll per k (measured, tools/brunet_kbench.py on the C5 shape: unroll 2 where the unrolled live ranges
 // push the register count past an occupancy step; round 5, with the one-step divide, re-measured against 2 / 4 / 8
 // for every k (profiles/r05/brunet/kbench_unroll_rg.txt): 8 for k = 4, 6 (-2.5 %, -10 % hnum + wupd), 2 for k = 8
 // (-12 %), k = 2, 3, 9 tied)
-#ifndef NMFC_BR_UNROLL
-constexpr int br_unroll(int K) { return (K == 4 || K == 6) ? 8 : (K == 5 || K == 7 || K == 8 || K == 10) ? 2 : 4; }
-#else
-constexpr int br_unroll(int) { return NMFC_BR_UNROLL; }   // experiment builds (tools/build_variant.sh)
-#endif
+constexpr int br_unroll(int K) {   // NMFC_BR_UNROLL != 0: one unroll for every k (experiment builds)
+  return NMFC_BR_UNROLL != 0 ? NMFC_BR_UNROLL
+                             : (K == 4 || K == 6) ? 8 : (K == 5 || K == 7 || K == 8 || K == 10) ? 2 : 4;
+}
 
 template <int K, int RG>
 struct OperandTiles {
@@ -850,6 +820,8 @@ int br_run_k(nmfc_brunet* e, BrLane* L, const KJob& kj, int B, int R, const nmfc
 }  // namespace
 
 extern "C" {
+
+const char* nmfc_build_tuning_brunet(void) { return NMFC_TUNING_BRUNET; }
 
 void nmfc_brunet_default_opts(nmfc_brunet_opts* o) {
   memset(o, 0, sizeof *o);

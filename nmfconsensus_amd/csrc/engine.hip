@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -133,37 +134,10 @@ enum { KID_WTA = 0, KID_HUPD = 1, KID_AHTW = 2, KID_INIT = 3, KID_OTHER = 4, KID
 // tail kernels apply as soon as the live restarts fit their blocks.  Placement never changes a result bit
 // (DESIGN.md "Determinism").
 constexpr int WTA_NPT = 4;
-#ifndef NMFC_AHTW_NBUF
-#define NMFC_AHTW_NBUF 2
-#endif
-#ifndef NMFC_AHTW_LATE
-#define NMFC_AHTW_LATE 1
-#endif
-#ifndef NMFC_NARROW_NBUF
-#define NMFC_NARROW_NBUF 16
-#endif
 constexpr int NARROW_NBUF = NMFC_NARROW_NBUF;      // LDS ring depth of the narrow (tail) W^T A kernel (16: +2 % on the R = 25 shard)
-#ifndef NMFC_WTA_MID_NBUF
-#define NMFC_WTA_MID_NBUF 3
-#endif
-#ifndef NMFC_WTA_MID_MINW
-#define NMFC_WTA_MID_MINW 1
-#endif
-#ifndef NMFC_WTA_MID_GREG
-#define NMFC_WTA_MID_GREG 1
-#endif
 constexpr bool WTA_MID_GREG = NMFC_WTA_MID_GREG != 0;   // 2-panel W^T A tile: 2 x 4 waves, Gram chains in registers
-#ifndef NMFC_SMALL_NW8
-#define NMFC_SMALL_NW8 1
-#endif
 constexpr bool SMALL_NW8 = NMFC_SMALL_NW8 != 0;    // k_small_mu with eight waves where m_pad % 256 == 0
-#ifndef NMFC_WTA_GREG
-#define NMFC_WTA_GREG 1
-#endif
 constexpr bool WTA_GREG = NMFC_WTA_GREG != 0;      // 4-panel W^T A tiles: diagonal Gram blocks from the tile's W registers
-#ifndef NMFC_WTA_W16
-#define NMFC_WTA_W16 1
-#endif
 constexpr bool WTA_W16 = NMFC_WTA_W16 != 0 && WTA_GREG;   // the 4-panel x 128-sample W^T A tile on 16 waves (4 per SIMD)
 constexpr int WTA_MID_NBUF = NMFC_WTA_MID_NBUF;    // ring depth of the 2-panel W^T A tile
 constexpr int WTA_MID_MINW = NMFC_WTA_MID_MINW;    // its launch-bounds waves per SIMD (4: two workgroups per CU)
@@ -587,6 +561,8 @@ struct TimedLaunch {
 extern "C" {
 
 const char* nmfc_last_error(void) { return g_err.c_str(); }
+
+const char* nmfc_build_tuning(void) { return NMFC_TUNING_MU; }
 const char* nmfc_version(void) { return "nmfconsensus_amd 0.2 (gfx950, fp64 MFMA)"; }
 
 void nmfc_default_opts(nmfc_sweep_opts* o) {
@@ -767,6 +743,12 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       set_err("nmfc_engine_run: k=%d unsupported (need 2 <= k <= min(%d, m, n))", ks[q], KMAX);
       return -1;
     }
+    // k_init walks a restart's m k + k n draws with 32-bit draw indices (one chunk of up to 31 x 32 past the end)
+    if ((long)m * ks[q] + (long)ks[q] * n + 31L * 32 >= (long)INT_MAX) {
+      set_err("nmfc_engine_run: m k + k n = %ld draws per restart exceeds the init kernel's 32-bit index range",
+              (long)m * ks[q] + (long)ks[q] * n);
+      return -1;
+    }
   }
   if (opts.maxiter < 0) {
     set_err("nmfc_engine_run: maxiter must be >= 0");
@@ -820,9 +802,11 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
   // the stop rule only, so a job takes the same path -- and gives the same bits -- in any batch)
   const bool small = e->small_ok && e->m_pad <= 1024 && n <= 64 && opts.stop_rule != NMFC_STOP_TOLX;
   std::vector<SmallBlock> sblocks;
-  // ... and there, a restart the solo kernel takes (rank <= 4, nmfc_mu_solo_fits) runs on one workgroup of its own
-  // (k_solo_mu, the kernel of the single-restart drop-in), the others in k_small_mu blocks; the choice is a function
-  // of (m, n, k) only, so a job gives the same bits in any batch, through nmf_mu and on any number of GPUs
+  // ... and there, a restart the solo kernels take (rank 2..8 on gct-sized shapes, nmfc_mu_solo_fits: k_solo_mu for
+  // ranks 2..4, k_solo8_mu for 5..8) runs on one workgroup of its own, the others in k_small_mu blocks; the choice is a
+  // function of (m, n, k) only, so a job gives the same bits in any batch and on any number of GPUs.  Through the
+  // single-restart nmf_mu drop-in the bits are the same for ranks 2..4 only (the drop-in runs k_solo_mu there); it
+  // runs ranks 5..8 on k_team_mu (faster for one restart), whose sums run in another order
   std::vector<RestartInfo> blk_jobs, solo_jobs;
   for (const RestartInfo& r : all) (small && e->solo_ok && nmfc_mu_solo_fits(m, n, r.k) ? solo_jobs : blk_jobs).push_back(r);
   Packing pk = small ? pack_small(blk_jobs, sblocks) : pack(all);

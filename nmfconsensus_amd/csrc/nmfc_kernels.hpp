@@ -15,6 +15,7 @@
 
 #include <type_traits>
 
+#include "nmfc_tuning.hpp"
 #include "rmt.hpp"
 
 namespace nmfc {
@@ -81,9 +82,6 @@ __device__ __forceinline__ int xcd_item(int b, int nblocks) {
 // ---------------------------------------------------------------------------------------------
 constexpr int BK2 = 16;
 constexpr int GT_NBUF = 3;
-#ifndef NMFC_GT_PRIO
-#define NMFC_GT_PRIO 0
-#endif
 constexpr bool GT_PRIO = NMFC_GT_PRIO != 0;   // raise the wave priority around each MFMA block (experiment)
 
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, uint32_t lds_addr, int voff, int soff) {
@@ -1124,20 +1122,11 @@ static __global__ __launch_bounds__(NTH, MINW) void k_hupdate(int iter, int maxi
 #undef NMFC_HUPD_CASE
 }
 
-#ifndef NMFC_AHTW_KSKIP
-#define NMFC_AHTW_KSKIP 1
-#endif
 constexpr bool AHTW_KSKIP = NMFC_AHTW_KSKIP != 0;   // A h^T: skip the K-padding half of the last stage (KHALF)
 
 // ---------------------------------------------------------------------------------------------
 // Item map of the A h^T kernels: (panel, gene tile) from the XCD-contiguous item index.
 // ---------------------------------------------------------------------------------------------
-#ifndef NMFC_AHTW_SP
-#define NMFC_AHTW_SP 32
-#endif
-#ifndef NMFC_AHTW_SG
-#define NMFC_AHTW_SG 4
-#endif
 __device__ __forceinline__ void ahtw_map(int item, int npanels, int ngt, int& p, int& gt) {
   // bands of SP panels, gene super-tiles of SG: neighbours share operands in L2
   const int SP = NMFC_AHTW_SP, SG = NMFC_AHTW_SG;
@@ -1358,13 +1347,7 @@ void k_ahtw4(int iter, const double* __restrict__ H, long n_pad, const double* _
 // Deterministic: every reduction order is a function of (m, n) only, so a job gives the same bits in
 // any block and any batch.
 // ---------------------------------------------------------------------------------------------
-#ifndef NMFC_SMALL_PF
-#define NMFC_SMALL_PF 8   // k-steps of A rows in flight in the G phase of k_small_mu
-#endif
 constexpr int SMALL_PF = NMFC_SMALL_PF;
-#ifndef NMFC_SMALL_FPF
-#define NMFC_SMALL_FPF 8   // F steps (4 gene blocks each) of A columns in flight
-#endif
 constexpr int SMALL_FPF = NMFC_SMALL_FPF;
 constexpr int SMALL_NW = 4;
 constexpr int SMALL_MAXR = 8;   // restarts per 16-column block (k >= 2)

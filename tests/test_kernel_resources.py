@@ -22,9 +22,10 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 SOLO_SPILLS = {
     "k_solo_muILi10ELi2ELi0ELi0ELi0ELb0E": 10,   # k = 2 x 40 samples, single restart (the nmf_mu drop-in)
     "k_solo_muILi10ELi2ELi0ELi0ELi0ELb1E": 24,   # the same, batched job loop (C1 / C2)
-    "k_solo_muILi10ELi4ELi0ELi0ELi2ELb1E": 1,    # k = 4 x 40, two gene steps in LDS, batched
     "k_solo_muILi8ELi3ELi0ELi0ELi0ELb1E": 2,     # k = 3 x 32, batched
-    "k_solo_muILi10ELi4ELi0ELi0ELi2ELb1E": 3,    # k = 4 x 40, batched beside k_small_mu blocks
+    # k = 4 x 40, two gene steps in LDS, batched: ONE instantiation serves the fused solo launch (C1 / C2) and the
+    # per-rank launches beside k_small_mu blocks (measured 3 spilled VGPRs, ROCm 7.2 hipcc, round 6)
+    "k_solo_muILi10ELi4ELi0ELi0ELi2ELb1E": 3,
     "k_solo_batchILi10E": 37,                    # every rank x 40 samples in one launch (the rank-2 body's edge)
 }
 
@@ -99,3 +100,44 @@ def test_brunet_divide_op_count_matches_isa():
         n_f64 = sum(1 for o in ops if o.startswith("v_") and "f64" in o and not o.startswith("v_mfma"))
         assert n_rcp > 0, kern
         assert n_f64 == n_rcp * (2 * k + BRUNET_DIV_OPS), (kern, n_f64, n_rcp)
+
+
+def _tuning_defaults():
+    import re
+    txt = open(os.path.join(CSRC, "nmfc_tuning.hpp")).read()
+    return dict(re.findall(r"#ifndef (NMFC_\w+)\n#define \1 (.+?)(?:\s*//[^\n]*)?\n#endif", txt))
+
+
+def test_tuning_switches_live_in_one_header():
+    """Every compile-time A/B switch is declared in csrc/nmfc_tuning.hpp; no other product source
+    opens its own #ifndef NMFC_* default, and the product build passes no -D."""
+    import re
+    defaults = _tuning_defaults()
+    assert len(defaults) >= 28, sorted(defaults)
+    for f in os.listdir(CSRC):
+        if f == "nmfc_tuning.hpp" or not f.endswith((".hip", ".hpp", ".cpp")):
+            continue
+        txt = open(os.path.join(CSRC, f)).read()
+        assert not re.search(r"#\s*if(n?def)\s+NMFC_|defined\s*\(\s*NMFC_", txt), f
+    build_src = open(os.path.join(ROOT, "nmfconsensus_amd", "build.py")).read()
+    assert '"-D' not in build_src and "'-D" not in build_src
+
+
+def test_product_build_uses_tuning_defaults():
+    """The built library reports, per translation unit, the values its switches had: they must be the header's
+    defaults, so an experiment build (tools/build_variant.sh) can never ship.  Loads the .so; no GPU call."""
+    import ctypes
+    so = os.path.join(ROOT, "nmfconsensus_amd", "lib", "libnmf.so")
+    if not os.path.exists(so):
+        pytest.skip("libnmf.so not built")
+    lib = ctypes.CDLL(so)
+    defaults = _tuning_defaults()
+    seen = set()
+    for fn in ("nmfc_build_tuning", "nmfc_build_tuning_brunet"):
+        f = getattr(lib, fn)
+        f.restype = ctypes.c_char_p
+        got = dict(kv.split("=", 1) for kv in f().decode().split(";"))
+        for k, v in got.items():
+            assert defaults[k] == v, (fn, k, v, defaults[k])
+        seen |= set(got)
+    assert seen == set(defaults), set(defaults) ^ seen
