@@ -184,3 +184,36 @@ def test_c5_full_size_stop_rule_vs_oracle():
     kf = int(g["c5_W_full_k"])
     assert relfro(r.W[ks.index(kf)], g["c5_W_full"]) < TOL
     assert r.counts.shape == (len(ks), n, n)
+
+
+def test_c5_four_restarts_per_k_multilane_vs_oracle():
+    """BASELINE configs[4] at full size, R = 4 restarts of every k = 2..10 (36 jobs: tests/golden/golden_c5.npz c5_*_all,
+    the Brunet oracle on every job, make_golden_c5.py) run as ONE multi-lane sweep (the default 4 lanes: k batches on
+    four host threads and streams, as the C5 bench runs): iterations, labels, the consensus counts of the 4 restarts
+    and the consensus bit-exact for every k, every job's H within 1e-9.  (9 -> 36 pinned jobs.)"""
+    import hashlib
+    import os
+    from conftest import ROOT
+    from nmfconsensus_amd.brunet import BrunetEngine
+    from nmfconsensus_amd.synthetic import planted_matrix
+    path = os.path.join(ROOT, "tests", "golden", "golden_c5.npz")
+    with np.load(path, allow_pickle=False) as z:
+        g = {k: z[k] for k in z.files}
+    if "c5_R" not in g:
+        pytest.skip("golden_c5.npz without the R = 4 set")
+    A = planted_matrix(int(g["c5_m"]), int(g["c5_n"]))
+    assert hashlib.sha256(np.ascontiguousarray(A).tobytes(order="F")).hexdigest() == str(g["c5_A_sha256"])
+    ks = [int(k) for k in g["c5_ks"]]
+    R = int(g["c5_R"])
+    with BrunetEngine(A) as eng:
+        r = eng.run(ks, R, maxiter=int(g["c5_maxiter"]), seed=int(g["c5_rseed"]), stopconv=int(g["c5_stopconv"]),
+                    stopfreq=int(g["c5_stopfreq"]), want_factors=True)
+    assert np.array_equal(r.iters.reshape(len(ks), R), g["c5_iters_all"]), (r.iters, g["c5_iters_all"])
+    for i, k in enumerate(ks):
+        L = g["c5_labels_all"][i].astype(np.int32)
+        assert np.array_equal(r.labels[i * R:(i + 1) * R], L), k
+        C = sum((l[:, None] == l[None, :]).astype(np.int32) for l in L)
+        assert np.array_equal(r.counts[i], C), k
+        assert np.array_equal(r.consensus[i], C / R), k
+        for q in range(R):
+            assert relfro(r.H[i * R + q], g[f"c5_Hall_k{k}"][q]) < TOL, (k, q)
