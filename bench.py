@@ -36,8 +36,10 @@ FP64_VALU_PEAK_TOPS = FP64_MFMA_PEAK_TFLOPS / 2
 # (2 FMA) + mul + residual FMA + correction FMA = 6; 8 with the second Newton step of rounds 1-4), k FMAs
 # accumulating W^T Q or Q H^T
 BRUNET_DIV_OPS = 6
-# restart groups for the whole job on one GPU (the default C3 line): the fastest measured policy
-N1_GROUPS = 2
+# restart groups for the whole job on one GPU (the default C3 line): the fastest measured policy (with
+# the stream-K W^T A tile one group is fastest -- 500.7 vs 475.5 restarts/s for three, whose persistent launches queue behind
+# each other; before it, three groups were +1.9 %)
+N1_GROUPS = 1
 
 
 def brunet_valu_ops_per_element(k: int) -> int:

@@ -304,6 +304,9 @@ struct nmfc_engine {
   DevBuf teamG, teamSW, teamFlag;   // k_team_mu: partial buffers, per-workgroup flags (+ the error word)
   DevBuf solojobs;                  // batched k_solo_mu jobs (small shapes, rank <= 4)
   bool narrow_lc = true;            // env NMFC_NARROW_LC=0: the one-wave narrow W^T A kernel
+  bool wta_sk = true;               // env NMFC_WTA_SK=0: the big W^T A tile one item per workgroup (no stream-K)
+  DevBuf skfix, skflag;             // k_wta2_sk: per-range hand-off slots and flags (flags zeroed once)
+  unsigned sk_epoch = 0;            // k_wta2_sk launches so far (the flag value of the current launch)
   bool gram_model = true;           // env NMFC_GRAM_MODEL=0: the tile cost model without the Gram workgroups
   bool solo_ok = true;              // env NMFC_SOLO=0: no solo kernel (every small-shape restart in k_small_mu blocks)
   hipStream_t aux[4] = {nullptr, nullptr, nullptr, nullptr};   // the solo launches (one per kernel rank: 2, 3, 4, 8)
@@ -353,6 +356,21 @@ struct TileChoice {
   bool ahtw_small;  // 64-gene A h^T tiles
 };
 
+// The stream-K big tile (k_wta2_sk): 16-wave GREG tiles (ntj >= 4), NMFC_WTA_SK not 0.  Its cost per round of items
+// against the one-item-per-workgroup kernel's (hand-offs, per-piece prologues; tools/kvar.hip: 3.34 vs 3.51 ms at the
+// C3 full-load grid of 6.72 rounds, i.e. ~1 % above the ideal 6.72 / 7 of the unsplit form's time)
+constexpr double WTA_SK_COST = 1.01;
+bool sk_big_ok(const nmfc_engine* e, int ntj) { return e->wta_sk && WTA_W16 && ntj >= 4; }
+// ... and its grid condition: at least one whole round of items, and every workgroup's even share of the stages at least
+// one item long (so an item is cut into at most two pieces: k_wta2_sk's contract)
+bool sk_big_fits(const nmfc_engine* e, long ngroups, int ntj) {
+  const long ipc = ngroups * ntj, nitems = ipc * e->nsplit;
+  const long nst_full = e->kchunk / 16, nst_last = (e->m_pad - (long)(e->nsplit - 1) * e->kchunk) / 16;
+  const long nst_max = e->nsplit > 1 ? nst_full : nst_last;
+  const long S = ipc * (e->nsplit - 1) * nst_full + ipc * nst_last;
+  return nitems >= e->ncu && S >= (long)e->ncu * nst_max;
+}
+
 TileChoice choose_tiles(const nmfc_engine* e, int np_live, int ntj) {
   const long ns = e->nsplit, cu = e->ncu;
   const long np = std::max(np_live, 1);
@@ -365,14 +383,17 @@ TileChoice choose_tiles(const nmfc_engine* e, int np_live, int ntj) {
     double wgs;
     long slots;
     double t;
-  } cands[4] = {{0, (double)(ns * ((np + 3) / 4) * ntj), cu, 2.0},
+  } cands[4] = {{0, (double)(ns * ((np + 3) / 4) * ntj), cu, 2.0 * WTA_SK_COST},
                 {3, (double)(ns * ((np + 1) / 2) * ntj), cu, 1.0},
                 {1, (double)(ns * np) * (2 * ntj + (e->gram_model ? 0.75 : 0.0)), 3 * cu, 0.8},
                 {2, (double)(ns * np) * (4 * ntj + (e->gram_model ? 1.5 : 0.0)), 4 * cu, 0.6}};
   TileChoice tc{0, false};
   double best = 1e300;
   for (const Cand& c : cands) {
-    const double est = std::ceil(c.wgs / (double)c.slots) * c.t;
+    // the big tile in its stream-K form (k_wta2_sk, from one whole round of items on) takes wgs / slots rounds, not
+    // ceil(wgs / slots): the last round's items are split over every CU
+    const bool sk = c.id == 0 && sk_big_ok(e, ntj) && sk_big_fits(e, (np + 3) / 4, ntj);
+    const double est = (sk ? c.wgs / (double)c.slots : std::ceil(c.wgs / (double)c.slots)) * c.t;
     if (est < best - 1e-9) {
       best = est;
       tc.wta = c.id;
@@ -611,6 +632,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_SMALL")) e->small_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SOLO")) e->solo_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_NARROW_LC")) e->narrow_lc = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_WTA_SK")) e->wta_sk = atoi(s) != 0;
   if (const char* s = getenv("NMFC_GRAM_MODEL")) e->gram_model = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SMALL_KERNEL"))
     e->small_kernel = std::string(s) == "team" ? 1 : std::string(s) == "single" ? 2 : 0;
@@ -1094,6 +1116,18 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                  e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
                                  e->colinfo.as<ColInfo>(),
                                  e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
+          } else if (wta_big && sk_big_ok(e, ntj) && sk_big_fits(e, pk.npanels / WTA_NPT, ntj)) {
+            // stream-K form: ncu persistent workgroups, whole rounds of items then the rest split evenly (bit-identical
+            // to the one-item-per-workgroup tile: the same MFMA chains, handed over at a stage boundary)
+            if (!e->skflag.p) {
+              if (e->skfix.ensure(sizeof(double) * SK_FIX * e->ncu) || e->skflag.ensure(sizeof(unsigned) * e->ncu)) return -1;
+              HCHECK(hipMemsetAsync(e->skflag.p, 0, sizeof(unsigned) * e->ncu, st));
+            }
+            const SkArgs a{e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, pk.npanels / WTA_NPT, ntj, e->kchunk,
+                           e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
+                           e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total,
+                           e->skfix.as<double>(), e->skflag.as<unsigned>(), ++e->sk_epoch, e->nsplit};
+            hipLaunchKernelGGL(k_wta2_sk<GT_NBUF>, dim3(e->ncu), dim3(SK_THREADS), 0, st, a);
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
             // ntj >= 4: 16 waves (4 per SIMD, 64 x 32 outputs each; round 5: +2 % over 8 waves at full load, every

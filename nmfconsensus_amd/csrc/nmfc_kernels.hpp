@@ -110,7 +110,11 @@ __device__ __forceinline__ void step_barrier() {
 // SPLIT (NBUF >= 3): the split-step form (below); false: each step computes its whole stage between the barriers
 // (one fragment set live instead of two: 24 VGPRs fewer at MB = 4, NB = 2, for the 16-wave tile).  Same order of
 // accumulation either way (kk = 0 then kk = 1 of every stage), so the same bits.
-template <int RP, int RQ, int WR, int WC, int NBUF = GT_NBUF, bool QBLK = false, bool GREG = false, bool SPLIT = true>
+// OPQ: the lane index comes from an opaque copy taken in bind() (per run), not from threadIdx.x: inside an outer loop
+// (k_wta2_sk's pieces) the lane-derived offsets then stay inside each run instead of being hoisted out of the outer
+// loop and held across every K loop.  The same values, the same code in the loop.
+template <int RP, int RQ, int WR, int WC, int NBUF = GT_NBUF, bool QBLK = false, bool GREG = false, bool SPLIT = true,
+          bool OPQ = false>
 struct GTile {
   static_assert(NBUF >= 2 && NBUF <= 16, "ring of 2..16 stages");
   static constexpr int NW = WR * WC;
@@ -131,11 +135,17 @@ struct GTile {
   __amdgpu_buffer_rsrc_t rp, rq;
   int voff[PPW];
   int qkm;
+  int tix = 0;  // OPQ: the opaque lane index (bind)
   int wo = 0;   // wave offset: this tile's waves are wo .. wo + NW - 1 of the workgroup (several 1-wave tiles per workgroup)   // QBLK: bytes between consecutive K positions' blocks / 8 (= 8 * total rows); else 8
 
   // P rows are K-contiguous at P + row*ldp, Q rows at Q + row*ldq (doubles); QBLK: Q + (k/16)*16*ldq + row*16
+  __device__ __forceinline__ int lane_ix() const { return OPQ ? tix : (int)(threadIdx.x & 63); }
   __device__ __forceinline__ void bind(const double* P, long ldp, const double* Q, long ldq, int kend) {
-    const int w = wave_id() - wo, l = threadIdx.x & 63;
+    if constexpr (OPQ) {
+      tix = lane_id();
+      asm volatile("" : "+v"(tix));
+    }
+    const int w = wave_id() - wo, l = lane_ix();
     rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(P), 0, (int)(RP * ldp * 8), 0x00020000);
     rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Q), 0, QBLK ? (int)((long)kend * ldq * 8) : (int)(RQ * ldq * 8),
                                            0x00020000);
@@ -183,7 +193,7 @@ struct GTile {
     d2 a[MB], b[NB];
   };
   __device__ __forceinline__ void load_frag(const char* __restrict__ st, int kk, Frag& f) const {
-    const int w = wave_id() - wo, l = threadIdx.x & 63;
+    const int w = wave_id() - wo, l = lane_ix();
     const int wr = w / WC, wc = w % WC;
     const int fr = l & 15, g = l >> 4;
     const char* sp = st + (wr * (RP / WR) + fr) * 128;
@@ -698,6 +708,319 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
   }
   if constexpr (GREG) {
     if (tl.gi >= 0) put_gram(64 * (w / WC) + 16 * tl.gi, 64 * (w / WC) + 16 * tl.gj, tl.gacc);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1 stream-K form of the 16-wave 4-panel x 128-sample W^T A tile (round 6).  The big tile's grid is nsplit x ng x
+// ntj items of up to kchunk / 16 stages each; as one workgroup per item (one per CU: 144 KiB of LDS) the launch takes
+// ceil(items / CUs) rounds for items / CUs rounds of work (C3 at full load: 1 720 items = 6.72 rounds, the short last
+// chunk makes it 6.56 rounds of work for 7 rounds of time).  Here G <= #CU persistent workgroups each take an equal
+// contiguous range of the S stages of all items (in the item order of k_wta2, ranges XCD-contiguous); a range starts
+// and ends anywhere inside an item, so an item is cut at a stage boundary into at most two pieces (G <= S / longest
+// item).  The canonical K order is kept exactly: the first piece accumulates stages [0, x) from zero, stores its
+// accumulators (G tile and register Gram chain, fp64 stores are exact) and publishes them; the second piece loads them
+// and continues the same MFMA chains over [x, end) -- the same chain, instruction for instruction, as one workgroup
+// running the whole item, so G and the Gram partials are bit-identical to k_wta2's (tools/kvar.hip checks it).
+// Deadlock freedom without any assumption on dispatch order: every range runs its first-piece (start) item FIRST
+// and its continuation LAST, and a continuation waits a bounded time; if the start piece has not been published by
+// then (its workgroup not yet dispatched), it recomputes the item from stage 0 -- the same bits again, only slower.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility; cdna_hip_programming.md split-K recipe): plain stores ->
+// every wave vmcnt(0) -> barrier -> lane 0 agent release fence -> vmcnt(0) -> relaxed agent flag store (= epoch of
+// this launch); reader lane 0 relaxed agent poll -> agent acquire fence -> vmcnt(0) -> barrier -> plain loads.
+// fix: G slots of SK_FIX doubles (9 d4 per lane: the 8 accumulator blocks and the Gram chain); flags: G words.
+// ---------------------------------------------------------------------------------------------
+constexpr int SK_THREADS = 1024;
+constexpr long SK_FIX = 9L * 4 * SK_THREADS;   // doubles per range slot
+constexpr int SK_POLLS = 256;                  // x s_sleep 127 (~3.4 us each): ~0.9 ms before recomputing
+
+// A wave-uniform copy of a value held in VGPRs (device-function arguments arrive in VGPRs): SGPR operands for the
+// buffer resources and soffsets of the K loop (a VGPR resource would wrap every buffer access in a waterfall loop).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ long uni(long v) {
+  const unsigned long long u = (unsigned long long)v;
+  return (long)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((int)(u & 0xffffffffu)));
+}
+template <class P>
+__device__ __forceinline__ P* uni(P* p) {
+  return reinterpret_cast<P*>(uni(reinterpret_cast<long>(p)));
+}
+// An SGPR value the compiler may not treat as loop-invariant (an empty asm that "redefines" it): what is computed from
+// it stays inside the loop instead of being hoisted and held in registers across the whole loop.
+template <class V>
+__device__ __forceinline__ V opaque(V v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
+struct SkArgs {   // the launch's operands: k_wta2_sk's only kernel argument (offset 0 of the kernarg segment)
+  const double* W;
+  const double* Acm;
+  long m_pad;
+  int ngroups, ntj, kchunk;
+  const int* prb;
+  const int* pre;
+  const RestartInfo* ri;
+  const ColInfo* ci;
+  const int* stop_iter;
+  double* Gpart;
+  long g_ld, g_split;
+  double* SWpart;
+  long sw_total;
+  double* fix;
+  unsigned* flags;
+  unsigned epoch;
+  int nsplit;
+};
+typedef const SkArgs __attribute__((address_space(4)))* SkArgsK;   // the kernarg copy, read by scalar loads
+
+// The kernarg segment as an opaque pointer: every operand is re-read (s_load) where it is used, instead of being held
+// in SGPRs across the whole piece loop -- the K loop then keeps k_wta2's SGPR and VGPR budget (a first form spilled).
+__device__ __forceinline__ SkArgsK sk_args() {
+  unsigned long long u = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(u));
+  return (SkArgsK)u;
+}
+
+// One piece of the stream-K range: item `item`, stages [s0, s1); mode 0 whole item, 1 start piece (publish its
+// chains in slot r), 2 continuation (of slot r - 1).  Every operand is re-read through opaque() per piece, so the
+// compiler cannot hoist per-piece scalars (buffer resources, row offsets of the eight K-loop instantiations) out of the
+// piece loop and hold them all at once: the K loop keeps k_wta2's register budget (a first form spilled).
+template <int NBUF, bool NOWAIT>
+__device__ __forceinline__ void wta_sk_piece(int r, int item_in, int s0_in, int s1_in, int mode_in,
+                                             char* __restrict__ smem) {
+  constexpr int NPT = 4, RQ = 128, WC = 4;
+  using T = GTile<64 * NPT, RQ, 4, WC, NBUF, true, true, true, true>;
+  SkArgsK A = sk_args();
+  const double* W = A->W;
+  const double* Acm = A->Acm;
+  const long m_pad = A->m_pad;
+  const int ngroups = A->ngroups, ntj = A->ntj, kchunk = A->kchunk;
+  const int* prb = A->prb;
+  const int* pre = A->pre;
+  const RestartInfo* ri = A->ri;
+  const ColInfo* ci = A->ci;
+  const int* stop_iter = A->stop_iter;
+  r = uni(r);
+  const int item = uni(item_in), s0 = uni(s0_in), s1 = uni(s1_in), mode = uni(mode_in);
+  const unsigned epoch = A->epoch;
+  // lane-derived values are computed from an opaque copy of the lane index where they are used: hoisted out of the
+  // piece loop they would all be held across the K loop (one VGPR too many there)
+  auto lane = [] {
+    int v = lane_id();
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  int* need = reinterpret_cast<int*>(smem + T::LDS_BYTES);   // 28 Gram candidates
+  int* okw = need + 28;                                       // the continuation's "published" word
+  const int w = wave_id();
+  const int t = uni(item % ntj);
+  const int pg = uni((item / ntj) % ngroups);
+  const int s = uni(item / (ngroups * ntj));
+  bool live[NPT];
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < NPT; ++q) {
+    live[q] = panel_live(prb, pre, NPT * pg + q, ri, stop_iter, 0);
+    any = any || live[q];
+  }
+  if (!any) return;   // both pieces of a dead item see the same stop_iter: neither runs, nobody waits
+  const int tid = 64 * w + lane();
+  if (tid < 7 * NPT) {
+    int q, br, bc;
+    gram_cand<NPT>(tid, q, br, bc);
+    int nd = live[q];
+    if (nd && br != bc) {
+      const ColInfo c = ci[(long)(NPT * pg + q) * PANEL + 16 * bc];
+      nd = (c.k > 0 && c.lc0 < 16 * bc);
+    }
+    need[tid] = nd;
+  }
+  unsigned* flags = A->flags;
+  double* fix = A->fix;
+  if (mode == 2 && tid == 0) {
+    int ok = 0;
+    for (int i = 0; i < (NOWAIT ? 0 : SK_POLLS); ++i) {
+      if (__hip_atomic_load(flags + (r - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) {
+        ok = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(127);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *okw = ok;
+  }
+  const int kbeg = s * kchunk;
+  const long ldq = (long)ntj * RQ;
+  const double* Q = Acm + (long)kbeg * ldq + (long)t * RQ * 16;
+  T tl;
+  tl.zero();
+  __syncthreads();   // need[] and okw visible
+  // continuation: the chains come back from slot r - 1 in run()'s pre() hook, after the prologue's first DMA issue (held
+  // in registers only from there on, where the K loop holds them anyway); not published: the whole item from stage 0
+  const bool cont = mode == 2 && uni(*okw) != 0;
+  const int resume = uni(cont ? s0 : (mode == 2 ? 0 : s0));
+  auto load_chains = [&] {
+    if (cont) {
+      const double* src = fix + (long)(r - 1) * SK_FIX + 4L * (64 * w);
+      const int ln = lane();
+#pragma unroll
+      for (int mb = 0; mb < T::MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < T::NB; ++nb)
+          tl.acc[mb][nb] = *reinterpret_cast<const d4*>(src + ((long)(mb * T::NB + nb) * SK_THREADS + ln) * 4);
+      tl.gacc = *reinterpret_cast<const d4*>(src + (8L * SK_THREADS + ln) * 4);
+    }
+    return true;
+  };
+  {
+    const int wr = w / WC, wc = w % WC;
+    int gi = -1, gj = -1, kth = 0;
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {   // as k_wta2 (GREG, WC = 4)
+      const int cand = c < 4 ? 4 * wr + c : 4 * NPT + 3 * wr + (c - 4);
+      if (cand % ntj != t) continue;
+      if (wc == ((t + wr + 2 * kth) & 3) && need[cand]) {
+        gi = c < 4 ? c : c - 4;
+        gj = c < 4 ? c : c - 3;
+      }
+      ++kth;
+    }
+    tl.gi = __builtin_amdgcn_readfirstlane(gi);
+    tl.gj = __builtin_amdgcn_readfirstlane(gj);
+  }
+  const double* P = W + (long)pg * 64 * NPT * m_pad + kbeg;
+  auto go = [&](auto gc) {
+    tl.template run<0, 2, decltype(gc)::value>(P, m_pad, Q, ldq, BK2 * resume, BK2 * s1, smem, load_chains,
+                                               [](const char*) {}, [] {});
+  };
+  switch (tl.gi < 0 ? -1 : 4 * tl.gi + tl.gj) {
+    case 0: go(std::integral_constant<int, 0>{}); break;
+    case 5: go(std::integral_constant<int, 5>{}); break;
+    case 10: go(std::integral_constant<int, 10>{}); break;
+    case 15: go(std::integral_constant<int, 15>{}); break;
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 6: go(std::integral_constant<int, 6>{}); break;
+    case 11: go(std::integral_constant<int, 11>{}); break;
+    default: go(std::integral_constant<int, -1>{}); break;
+  }
+  if (mode == 1) {   // publish the start piece's chains for range r + 1
+    // lane index by mbcnt and the wave index in an SGPR: nothing derived from threadIdx.x is held across the K loop
+    A = sk_args();
+    fix = A->fix;
+    flags = A->flags;
+    double* dst = fix + (long)r * SK_FIX + 4L * (64 * w);
+    const int ln = lane();
+#pragma unroll
+    for (int mb = 0; mb < T::MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < T::NB; ++nb)
+        *reinterpret_cast<d4*>(dst + ((long)(mb * T::NB + nb) * SK_THREADS + ln) * 4) = tl.acc[mb][nb];
+    *reinterpret_cast<d4*>(dst + (8L * SK_THREADS + ln) * 4) = tl.gacc;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (w == 0 && ln == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(flags + r, A->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  A = sk_args();   // re-read after the K loop
+  const long g_ld = A->g_ld, g_split = A->g_split;
+  double* out = A->Gpart + (long)s * g_split + (long)pg * 64 * NPT * g_ld + (long)t * RQ;
+  {   // T::row_of / T::col_of from the opaque lane
+    const int ln = lane();
+    const int r0 = (w / WC) * 64 + (ln >> 4), c0 = (w % WC) * (RQ / WC) + (ln & 15);
+#pragma unroll
+    for (int mb = 0; mb < T::MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < T::NB; ++nb)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) out[(long)(r0 + mb * 16 + 4 * reg) * g_ld + c0 + nb * 16] = tl.acc[mb][nb][reg];
+  }
+  if (tl.gi >= 0) {   // the restart-diagonal entries of the wave's Gram block (as k_wta2's put_gram)
+    const int ra = 64 * (w / WC) + 16 * tl.gi, rb = 64 * (w / WC) + 16 * tl.gj;
+    double* so = A->SWpart + (long)s * A->sw_total;
+    const ColInfo* cp = ci + (long)(NPT * pg + (ra >> 6)) * PANEL;
+    const int ln = lane();
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int lr = (ra & 63) + (ln >> 4) + 4 * reg;
+      const int lcn = (rb & 63) + (ln & 15);
+      const ColInfo cr = cp[lr];
+      if (cr.k == 0 || cr.lc0 != cp[lcn].lc0 || cp[lcn].k == 0) continue;
+      const int a = lr - cr.lc0, bq = lcn - cr.lc0;
+      so[cr.sq_off + a * cr.k + bq] = tl.gacc[reg];
+      so[cr.sq_off + bq * cr.k + a] = tl.gacc[reg];
+    }
+  }
+}
+
+// NOWAIT (tools/kvar.hip only): every continuation takes the recompute path (tests its bits)
+template <int NBUF = GT_NBUF, bool NOWAIT = false>
+static __global__ __launch_bounds__(SK_THREADS, 1) void k_wta2_sk(SkArgs args) {
+  using T = GTile<256, 128, 4, 4, NBUF, true, true, true, true>;
+  static_assert(T::NTH == SK_THREADS, "16 waves");
+  __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES + 128];
+  (void)args;   // read through sk_args() (the kernarg segment), see there
+  SkArgsK A = sk_args();
+  const int nsplit = A->nsplit;
+  const int G = gridDim.x;
+  const int r = __builtin_amdgcn_readfirstlane(xcd_item(blockIdx.x, G));
+  const int ipc = A->ngroups * A->ntj;
+  const int nitems = nsplit * ipc;
+  const int nst_full = A->kchunk / BK2;
+  const int nst_last = (int)((A->m_pad - (long)(nsplit - 1) * A->kchunk) / BK2);
+  const int nst_max = nsplit > 1 ? nst_full : nst_last;
+  const int c_last = ipc * (nsplit - 1);   // first item of the last chunk
+  auto nst_of = [&](int item) { return item >= c_last ? nst_last : nst_full; };
+  auto off = [&](int item) -> long {        // stage offset of an item in k_wta2's item order
+    return item <= c_last ? (long)item * nst_full : (long)c_last * nst_full + (long)(item - c_last) * nst_last;
+  };
+  auto locate = [&](long x, int& item, int& st) {
+    const long lc = (long)c_last * nst_full;
+    const int it = x < lc ? (int)(x / nst_full) : c_last + (int)((x - lc) / nst_last);
+    item = __builtin_amdgcn_readfirstlane(it);
+    st = __builtin_amdgcn_readfirstlane((int)(x - off(it)));
+  };
+  // whole rounds first, item k G + r in round k (the dispatch order of k_wta2: the items a round runs at once are
+  // neighbours that share their A chunk and W rows in L2); the items left after them -- between one and two rounds'
+  // worth, at least G x the longest item in stages -- are split evenly over the G workgroups (stream-K)
+  int D = (nitems / G - 1) * G;
+  if (D < 0) D = 0;
+  while (D > 0 && off(nitems) - off(D) < (long)G * nst_max) D -= G;
+  D = __builtin_amdgcn_readfirstlane(D);
+  const long base = off(D), S = off(nitems) - base;
+  const long b = base + S * r / G, e = base + S * (r + 1) / G;
+  int ib, sb, ie, se;
+  locate(b, ib, sb);
+  locate(e - 1, ie, se);
+  ++se;   // the range's piece of item ie is [0, se)
+  const bool head = sb > 0;                 // [sb, nst) of item ib: a continuation of range r - 1's start piece
+  const bool tail = se < nst_of(ie);        // [0, se) of item ie: the start piece, published for range r + 1
+  const int f0 = head ? ib + 1 : ib, f1 = tail ? ie - 1 : ie;   // whole items f0 .. f1 of the split part
+  const int nfull = f1 >= f0 ? f1 - f0 + 1 : 0;
+  const int ndp = D / G;
+  const int t0 = tail ? 1 : 0;
+  const int npieces = t0 + ndp + nfull + (head ? 1 : 0);
+  for (int pc = 0; pc < npieces; ++pc) {
+    // piece order: the start piece first (a later range waits for it), the whole rounds, the split part's whole items,
+    // the continuation last
+    int item, s0, s1, mode;
+    if (pc < t0) {
+      item = ie, s0 = 0, s1 = se, mode = 1;
+    } else if (pc < t0 + ndp) {
+      item = (pc - t0) * G + r, s0 = 0, s1 = nst_of(item), mode = 0;
+    } else if (head && pc == npieces - 1) {
+      item = ib, s0 = sb, s1 = nst_of(ib), mode = 2;
+    } else {
+      item = f0 + pc - t0 - ndp, s0 = 0, s1 = nst_of(item), mode = 0;
+    }
+    __syncthreads();   // the previous piece's LDS ring, need[] and okw are free
+    wta_sk_piece<NBUF, NOWAIT>(r, item, s0, s1, mode, smem);
   }
 }
 

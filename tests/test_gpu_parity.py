@@ -304,6 +304,38 @@ def test_tile_shapes_bit_identical(oracle, n):
     assert relfro(ref.W[3], Wo) < TOL and relfro(ref.H[3], Ho) < TOL
 
 
+@pytest.mark.parametrize("m,R", [(4200, 160), (2000, 310)])
+def test_wta_stream_k_bit_identical(oracle, m, R):
+    """The big W^T A tile in its stream-K form (k_wta2_sk: whole rounds of items, then the rest split at stage boundaries
+    over every CU with the MFMA chains handed over) gives the bits of the one-item-per-workgroup kernel: W and H after
+    fixed iterations equal bit for bit with NMFC_WTA_SK=0.  m = 4200: three gene chunks, the last 128 genes long;
+    m = 2000: one chunk.  Both grids are large enough for the stream-K launch (>= one round of items, every share at
+    least one item long)."""
+    import os
+    from nmfconsensus_amd.nmf import Engine
+    rng = np.random.default_rng(m)
+    n, ks, T = 500, list(range(2, 11)), 6
+    A = np.asfortranarray(rng.random((m, n)) * 3.0)
+    runs = {}
+    try:
+        os.environ["NMFC_WTA_TILE"] = "big"
+        for sk in ("1", "0"):
+            os.environ["NMFC_WTA_SK"] = sk
+            with Engine(A) as eng:
+                runs[sk] = eng.run(ks, R, maxiter=T, seed=9, stop_rule=0, want_factors=True, want_counts=False)
+    finally:
+        os.environ.pop("NMFC_WTA_TILE", None)
+        os.environ.pop("NMFC_WTA_SK", None)
+    a, b = runs["1"], runs["0"]
+    for j in range(len(ks) * R):
+        assert np.array_equal(a.W[j], b.W[j]) and np.array_equal(a.H[j], b.H[j]), j
+    j = 5   # one restart against the oracle too
+    k = ks[j % len(ks)]
+    W0, H0 = oracle.init_restart(9 + j, m, n, k)
+    Wo, Ho, _ = oracle.nmf_mu(A, W0, H0, T, 0)
+    assert relfro(a.W[j], Wo) < TOL and relfro(a.H[j], Ho) < TOL
+
+
 def test_full_size_c3_shape_vs_oracle(oracle):
     # BASELINE config C3 shape (20000 x 500), k = 10, a few fixed iterations against the oracle
     from nmfconsensus_amd.nmf import Engine

@@ -45,6 +45,16 @@ def _usage(src):
     return out
 
 
+# engine kernels allowed a pinned spill count: k_wta2_sk (the stream-K big W^T A tile) reloads 2 VGPRs once per piece,
+# outside its K loops (test_wta_sk_k_loops_spill_free checks the loops themselves)
+ENGINE_SPILLS = {"k_wta2_sk": 2}
+
+
+def _short(mangled):
+    m = re.search(r"L\d+(k_\w+?)I|L\d+(k_\w+?)E", mangled)
+    return (m.group(1) or m.group(2)) if m else mangled
+
+
 OCC = {}   # kernel -> waves per SIMD its registers allow (filled by _usage)
 # the full-load MFMA tiles keep the occupancy their design rests on: A h^T three workgroups per CU
 # (four waves each: 3 per SIMD), the 16-wave W^T A tile one workgroup of 4 waves per SIMD
@@ -58,7 +68,7 @@ def test_no_register_spills():
         res = dict(zip(srcs, ex.map(_usage, srcs)))
     for src in ("engine.hip", "brunet.hip", "generic.hip"):
         assert res[src], f"no kernels found in {src}"
-        bad = {k: v for k, v in res[src].items() if v != (0, 0)}
+        bad = {k: v for k, v in res[src].items() if v != (0, 0) and v[0] > ENGINE_SPILLS.get(_short(k), -1)}
         assert not bad, f"{src}: spilling kernels {bad}"
     def allowed(name):
         return next((v for key, v in SOLO_SPILLS.items() if key in name), 0)
@@ -141,3 +151,33 @@ def test_product_build_uses_tuning_defaults():
             assert defaults[k] == v, (fn, k, v, defaults[k])
         seen |= set(got)
     assert seen == set(defaults), set(defaults) ^ seen
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_wta_sk_k_loops_spill_free():
+    """k_wta2_sk runs eight K-loop instantiations inside its piece loop: no scratch access may sit in any of those inner
+    loops (a first form reloaded a fragment offset every stage), and every inner loop carries the tile's MFMAs."""
+    with tempfile.TemporaryDirectory() as td:
+        s = os.path.join(td, "e.s")
+        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S",
+                            os.path.join(CSRC, "engine.hip"), "-o", s], capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = open(s).read().splitlines()
+    start = next(i for i, l in enumerate(lines) if re.match(r"^_Z\S*k_wta2_sk\S*:", l))
+    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+    depth, inner_mfma, inner_scratch, blocks = 0, 0, 0, 0
+    for l in lines[start:end]:
+        if re.match(r"^\.LBB\w+:", l):
+            m = re.search(r"Depth=(\d)", l)
+            depth = int(m.group(1)) if m else 0
+            blocks += depth >= 2
+            continue
+        m = re.match(r"^\s*; =>.*Loop Header: Depth=(\d)", l)
+        if m:
+            depth = int(m.group(1))
+            continue
+        if depth >= 2:
+            inner_mfma += "v_mfma_f64_16x16x4" in l
+            inner_scratch += "scratch_" in l
+    assert blocks > 0 and inner_mfma >= 8 * 32, (blocks, inner_mfma)
+    assert inner_scratch == 0, f"{inner_scratch} scratch accesses inside k_wta2_sk's K loops"

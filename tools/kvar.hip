@@ -565,10 +565,54 @@ int main(int argc, char** argv) {
       CK(hipMemcpy(dprb, pbs.data(), sizeof(int) * npanels, hipMemcpyHostToDevice));
       CK(hipMemcpy(dpre, pes.data(), sizeof(int) * npanels, hipMemcpyHostToDevice));
     }
+    // stream-K form (round 6): bit identity against the engine's big tile, the recompute path included
+    double* fixb = nullptr;
+    unsigned* flg = nullptr;
+    unsigned epoch = 0;
+    int ncu = 256;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    CK(hipMalloc(&fixb, sizeof(double) * SK_FIX * ncu));
+    CK(hipMalloc(&flg, sizeof(unsigned) * ncu));
+    CK(hipMemset(flg, 0, sizeof(unsigned) * ncu));
+    const long sk_stages = (long)ng * ntj * ((m_pad + 15) / 16);
+    const int gsk = (int)std::min<long>(ncu, sk_stages / (kchunk / 16));
+    auto SK = [&](int G, bool nowait) {
+      ++epoch;
+      const SkArgs a{W, Ablk, m_pad, ng, ntj, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, (long)sq,
+                     fixb, flg, epoch, nsplit};
+      if (nowait)
+        hipLaunchKernelGGL((k_wta2_sk<3, true>), dim3(G), dim3(SK_THREADS), 0, 0, a);
+      else
+        hipLaunchKernelGGL((k_wta2_sk<3>), dim3(G), dim3(SK_THREADS), 0, 0, a);
+    };
+    if (!pmc && ntj >= 4) {
+      const size_t gn = (size_t)nsplit * g_split, sn = (size_t)nsplit * sq;
+      std::vector<double> g1(gn), g2(gn), s1(sn), s2(sn);
+      auto grab = [&](std::vector<double>& g, std::vector<double>& sw, auto launch) {
+        CK(hipMemset(Gpart, 0xff, sizeof(double) * gn));
+        CK(hipMemset(SWpart, 0xff, sizeof(double) * sn));
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(g.data(), Gpart, sizeof(double) * gn, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(sw.data(), SWpart, sizeof(double) * sn, hipMemcpyDeviceToHost));
+      };
+      grab(g1, s1, [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); });
+      for (int G : {gsk, gsk / 2 + 1, 37}) {
+        for (int nw = 0; nw < 2; ++nw) {
+          grab(g2, s2, [&] { SK(G, nw == 1); });
+          printf("  stream-K G=%d%s vs engine big tile: G partials %s, Gram partials %s\n", G, nw ? " (recompute path)" : "",
+                 memcmp(g1.data(), g2.data(), sizeof(double) * gn) ? "DIFFER" : "bit-identical",
+                 memcmp(s1.data(), s2.data(), sizeof(double) * sn) ? "DIFFER" : "bit-identical");
+        }
+      }
+    }
     std::vector<std::pair<std::string, std::function<void()>>> warms;
     if (ntj >= 4) {
       warms = {
-          {"k_wta2 big 4x128 nbuf3 GREG (engine)", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true); }},
+          {"k_wta2 big 4x128 nbuf3 GREG (8 waves)", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true); }},
+          {"  16 waves, GREG (engine)", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); }},
+          {"  stream-K 16 waves GREG, G = CUs", [&] { SK(gsk, false); }},
+          {"  stream-K, recompute path (no hand-off)", [&] { SK(gsk, true); }},
           {"  Gram in LDS chains (round 3 form)", [&] { WA(4, 128, 4, 2, 1, 3, 1, true); }},
           {"  no Gram chains", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, false); }},
           {"  nbuf 2, LDS Gram", [&] { WA(4, 128, 4, 2, 1, 2, 1, true); }},
