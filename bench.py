@@ -244,7 +244,7 @@ def main():
     if args.groups > 0:
         G = args.groups
     elif world > 1:
-        G = 2 if (args.scaling == "strong" and je - jb >= 2) else 1
+        G = shard_groups(m, n, ks, jb, je, dev) if args.scaling == "strong" else 1
     else:
         G = N1_GROUPS if je - jb >= N1_GROUPS else 1
     if G > 8:
@@ -557,7 +557,7 @@ def bench_simulated_world(args, dev):
     stop_rule = {"fixed": 0, "ref_compat": 1, "argmax_stable": 2}[args.stop_rule]
     A_dev = torch.from_numpy(planted_matrix(m, n).T.copy()).to(dev)
     torch.cuda.synchronize()
-    G = args.groups if args.groups > 0 else 2
+    G = args.groups if args.groups > 0 else max(shard_groups(m, n, ks, *shard_range_(nk * R, r, W), dev) for r in range(W))
     grp = RestartGroups(a_device_ptr=A_dev.data_ptr(), shape=(m, n), device=dev.index, groups=G)
     part = torch.zeros((nk, n, n), dtype=torch.int32, device=dev)
     total = torch.zeros_like(part)
@@ -633,6 +633,25 @@ def bench_simulated_world(args, dev):
 def shard_range_(njobs, rank, world):
     from nmfconsensus_amd.distributed import shard_range
     return shard_range(njobs, rank, world)
+
+
+def shard_groups(m, n, ks, jb, je, dev):
+    """Restart groups for a strong-scaling shard (jobs jb..je-1 of the expand.grid list): 2 where the shard's full-load
+    W^T A grid stays below one round of the big tile on this GPU's CUs -- the engine then runs the one-item-per-workgroup
+    tile and a second group fills the partial rounds (R = 25 per GPU, the 8-GPU C3 shard: +1 to +2.4 %) -- else 1: the
+    stream-K tile already splits the last round over every CU, and two groups' persistent launches queue behind each
+    other (R = 50: 456.1 vs 443.1 restarts/s; R = 100: 477.8 vs 479.4, tied; profiles/r06/groups_sk/).  A speed choice
+    only; the packing estimate (columns = sum of k, 64 per panel, 4 panels per group) need not match the engine's exactly."""
+    import math
+    import torch
+    if je - jb < 2:
+        return 1
+    cols = sum(ks[j % len(ks)] for j in range(jb, je))
+    ngroups = math.ceil(math.ceil(cols / 64) / 4)
+    m_pad = -(-m // 128) * 128
+    items = ngroups * math.ceil(n / 128) * math.ceil(m_pad / 2048)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    return 1 if (math.ceil(n / 128) >= 4 and items >= ncu) else 2
 
 
 def dump_maps(path):
