@@ -305,7 +305,9 @@ struct nmfc_engine {
   DevBuf solojobs;                  // batched k_solo_mu jobs (small shapes, rank <= 4)
   bool narrow_lc = true;            // env NMFC_NARROW_LC=0: the one-wave narrow W^T A kernel
   bool wta_sk = true;               // env NMFC_WTA_SK=0: the big W^T A tile one item per workgroup (no stream-K)
-  DevBuf skfix, skflag;             // k_wta2_sk: per-range hand-off slots and flags (flags zeroed once)
+  bool wta_lastsum = false;         // env NMFC_WTA_LASTSUM=1: k_wta2_sk sums each tile's chunk partials (probe arm)
+  int sk_dp_xcd = 0;                // env NMFC_SK_DP_XCD=1: k_wta2_sk's whole rounds in XCD-contiguous blocks (probe)
+  DevBuf skfix, skflag, sktcnt;     // k_wta2_sk: per-range hand-off slots and flags (zeroed once), per-tile tickets
   unsigned sk_epoch = 0;            // k_wta2_sk launches so far (the flag value of the current launch)
   bool gram_model = true;           // env NMFC_GRAM_MODEL=0: the tile cost model without the Gram workgroups
   bool solo_ok = true;              // env NMFC_SOLO=0: no solo kernel (every small-shape restart in k_small_mu blocks)
@@ -633,6 +635,8 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_SOLO")) e->solo_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_NARROW_LC")) e->narrow_lc = atoi(s) != 0;
   if (const char* s = getenv("NMFC_WTA_SK")) e->wta_sk = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_WTA_LASTSUM")) e->wta_lastsum = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_SK_DP_XCD")) e->sk_dp_xcd = atoi(s) != 0;
   if (const char* s = getenv("NMFC_GRAM_MODEL")) e->gram_model = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SMALL_KERNEL"))
     e->small_kernel = std::string(s) == "team" ? 1 : std::string(s) == "single" ? 2 : 0;
@@ -1099,11 +1103,13 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
       const int grid_ahtw = lp * ngt_ahtw;
       for (int c = 1; c <= chunk; ++c) {
         const int iter = it + c;
+        int gsplit = e->nsplit;
         {
           // W^T A on the GTile core: 4-panel x 128-sample tiles (8 waves) while the grid fills the chip
           // at least twice, else 1-panel x 64-sample tiles (4 waves).  Both accumulate every entry in
           // the same canonical K order, so the switch never changes a bit.
           TimedLaunch tl(e, KID_WTA, iter % e->timing_stride == 0);
+          gsplit = e->nsplit;   // chunk partials k_hupdate sums (1 after a LASTSUM launch)
           if (narrow) {
             const int ntq = (int)(e->n_cols_pad / 16);
             if (e->narrow_lc)   // loader / consumer waves (bit-identical to the one-wave form)
@@ -1123,11 +1129,22 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
               if (e->skfix.ensure(sizeof(double) * SK_FIX * e->ncu) || e->skflag.ensure(sizeof(unsigned) * e->ncu)) return -1;
               HCHECK(hipMemsetAsync(e->skflag.p, 0, sizeof(unsigned) * e->ncu, st));
             }
+            const long tiles = (long)(pk.npanels / WTA_NPT) * ntj;
+            if (e->wta_lastsum && e->sktcnt.bytes < sizeof(unsigned) * tiles) {
+              if (e->sktcnt.ensure(sizeof(unsigned) * tiles)) return -1;   // fresh tickets: zero
+              HCHECK(hipMemsetAsync(e->sktcnt.p, 0, sizeof(unsigned) * tiles, st));
+            }
             const SkArgs a{e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, pk.npanels / WTA_NPT, ntj, e->kchunk,
                            e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
                            e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total,
-                           e->skfix.as<double>(), e->skflag.as<unsigned>(), ++e->sk_epoch, e->nsplit};
-            hipLaunchKernelGGL(k_wta2_sk<GT_NBUF>, dim3(e->ncu), dim3(SK_THREADS), 0, st, a);
+                           e->skfix.as<double>(), e->skflag.as<unsigned>(), ++e->sk_epoch, e->nsplit,
+                           e->sktcnt.as<unsigned>(), e->sk_dp_xcd};
+            if (e->wta_lastsum) {
+              hipLaunchKernelGGL((k_wta2_sk<GT_NBUF, false, true>), dim3(e->ncu), dim3(SK_THREADS), 0, st, a);
+              gsplit = 1;   // every tile's chunk partials summed into chunk slot 0
+            } else {
+              hipLaunchKernelGGL(k_wta2_sk<GT_NBUF>, dim3(e->ncu), dim3(SK_THREADS), 0, st, a);
+            }
           } else if (wta_big) {
             const int ng = pk.npanels / WTA_NPT;
             // ntj >= 4: 16 waves (4 per SIMD, 64 x 32 outputs each; round 5: +2 % over 8 waves at full load, every
@@ -1174,7 +1191,7 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
         {
           TimedLaunch tl(e, KID_HUPD, iter % e->timing_stride == 0);
           hipLaunchKernelGGL(k_hupdate<>, dim3(nact), dim3(NTH), 0, st, iter, opts.maxiter, opts.stop_rule,
-                             e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, e->nsplit,
+                             e->rinfo.as<RestartInfo>(), n, e->n_pad, e->Gpart.as<double>(), g_ld, g_split, gsplit, e->nsplit,
                              e->SWpart.as<double>(), sw_total, e->H[cur].as<double>(), e->SH.as<double>(),
                              e->stop_iter.as<int>(), e->stop_reason.as<int>(), e->unchanged.as<int>(),
                              e->classes.as<int>(), cls_ld, e->n_stopped.as<int>(), e->SHP.as<double>(),

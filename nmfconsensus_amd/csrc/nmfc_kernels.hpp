@@ -772,6 +772,8 @@ struct SkArgs {   // the launch's operands: k_wta2_sk's only kernel argument (of
   unsigned* flags;
   unsigned epoch;
   int nsplit;
+  unsigned* tcnt;   // LSUM: per-tile chunk-arrival counters (monotonic: nsplit arrivals per tile and launch)
+  int dp_xcd;       // whole rounds: 0 round-robin (item k G + r), 1 XCD-contiguous blocks (a speed / DVFS probe)
 };
 typedef const SkArgs __attribute__((address_space(4)))* SkArgsK;   // the kernarg copy, read by scalar loads
 
@@ -787,7 +789,11 @@ __device__ __forceinline__ SkArgsK sk_args() {
 // chains in slot r), 2 continuation (of slot r - 1).  Every operand is re-read through opaque() per piece, so the
 // compiler cannot hoist per-piece scalars (buffer resources, row offsets of the eight K-loop instantiations) out of the
 // piece loop and hold them all at once: the K loop keeps k_wta2's register budget (a first form spilled).
-template <int NBUF, bool NOWAIT>
+// LSUM (probe arm, NMFC_WTA_LASTSUM=1): the workgroup that writes a tile's last chunk partial sums
+// the tile's nsplit partials in chunk order -- k_hupdate's order, the same bits -- into chunk slot 0, so k_hupdate
+// reads one partial instead of nsplit.  Publication: every wave vmcnt(0) -> barrier -> lane 0 agent release -> ticket;
+// the ticket that completes the tile -> agent acquire -> barrier -> plain loads.
+template <int NBUF, bool NOWAIT, bool LSUM = false>
 __device__ __forceinline__ void wta_sk_piece(int r, int item_in, int s0_in, int s1_in, int mode_in,
                                              char* __restrict__ smem) {
   constexpr int NPT = 4, RQ = 128, WC = 4;
@@ -957,10 +963,56 @@ __device__ __forceinline__ void wta_sk_piece(int r, int item_in, int s0_in, int 
       so[cr.sq_off + bq * cr.k + a] = tl.gacc[reg];
     }
   }
+  if constexpr (LSUM) {
+    A = sk_args();   // everything from the kernarg copy and `item` again: nothing extra held across the K loop
+    const int nsplit = A->nsplit;
+    if (nsplit > 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int ntj2 = A->ntj, ng2 = A->ngroups;
+      const int tile = item % (ng2 * ntj2), pg2 = (item / ntj2) % ng2, t2 = item % ntj2;
+      if (w == 0 && lane() == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(A->tcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = (old + 1) % (unsigned)nsplit == 0;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *okw = last;
+      }
+      __syncthreads();
+      if (uni(*okw)) {   // the tile's partials, chunk 0 first, summed as k_hupdate sums them, into chunk slot 0
+        const long g_ld2 = A->g_ld, g_split2 = A->g_split;
+        double* base = A->Gpart + (long)pg2 * 64 * NPT * g_ld2 + (long)t2 * RQ;
+        const int ln = lane();
+        const int r0 = (w / WC) * 64 + (ln >> 4), c0 = (w % WC) * (RQ / WC) + (ln & 15);
+#pragma unroll
+        for (int mb = 0; mb < T::MB; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < T::NB; ++nb) {
+            double v[4];
+            double* e0 = base + (long)(r0 + mb * 16) * g_ld2 + c0 + nb * 16;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) v[reg] = e0[(long)4 * reg * g_ld2];
+            for (int c = 1; c < nsplit; ++c) {
+              double u[4];
+#pragma unroll
+              for (int reg = 0; reg < 4; ++reg) u[reg] = e0[(long)c * g_split2 + (long)4 * reg * g_ld2];
+#pragma unroll
+              for (int reg = 0; reg < 4; ++reg) v[reg] = v[reg] + u[reg];
+            }
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) e0[(long)4 * reg * g_ld2] = v[reg];
+          }
+      }
+    }
+  }
 }
 
 // NOWAIT (tools/kvar.hip only): every continuation takes the recompute path (tests its bits)
-template <int NBUF = GT_NBUF, bool NOWAIT = false>
+template <int NBUF = GT_NBUF, bool NOWAIT = false, bool LSUM = false>
 static __global__ __launch_bounds__(SK_THREADS, 1) void k_wta2_sk(SkArgs args) {
   using T = GTile<256, 128, 4, 4, NBUF, true, true, true, true>;
   static_assert(T::NTH == SK_THREADS, "16 waves");
@@ -970,6 +1022,9 @@ static __global__ __launch_bounds__(SK_THREADS, 1) void k_wta2_sk(SkArgs args) {
   const int nsplit = A->nsplit;
   const int G = gridDim.x;
   const int r = __builtin_amdgcn_readfirstlane(xcd_item(blockIdx.x, G));
+  // this workgroup's XCD (blocks b, b + 8, ... share one): its xcd_item range [xb, xb + xc) of the G ranges
+  const int xq = G >> 3, xrem = G & 7, xcd = blockIdx.x & 7;
+  const int xc = xq + (xcd < xrem ? 1 : 0), xb = xcd < xrem ? xcd * (xq + 1) : xrem * (xq + 1) + (xcd - xrem) * xq;
   const int ipc = A->ngroups * A->ntj;
   const int nitems = nsplit * ipc;
   const int nst_full = A->kchunk / BK2;
@@ -1013,14 +1068,19 @@ static __global__ __launch_bounds__(SK_THREADS, 1) void k_wta2_sk(SkArgs args) {
     if (pc < t0) {
       item = ie, s0 = 0, s1 = se, mode = 1;
     } else if (pc < t0 + ndp) {
-      item = (pc - t0) * G + r, s0 = 0, s1 = nst_of(item), mode = 0;
+      // whole rounds: round k is items k G .. k G + G - 1 (k_wta2's first rounds), workgroup r taking k G + r; or
+      // (dp_xcd) XCD-contiguous: the xc workgroups of an XCD walk the XCD's own block of ndp x xc items together, so an
+      // XCD stays on one chunk's A and neighbouring panel groups' W rows over several rounds -- bit-identical either
+      // way, a speed / L2-residency probe
+      item = A->dp_xcd ? ndp * xb + (pc - t0) * xc + (r - xb) : (pc - t0) * G + r;
+      s0 = 0, s1 = nst_of(item), mode = 0;
     } else if (head && pc == npieces - 1) {
       item = ib, s0 = sb, s1 = nst_of(ib), mode = 2;
     } else {
       item = f0 + pc - t0 - ndp, s0 = 0, s1 = nst_of(item), mode = 0;
     }
     __syncthreads();   // the previous piece's LDS ring, need[] and okw are free
-    wta_sk_piece<NBUF, NOWAIT>(r, item, s0, s1, mode, smem);
+    wta_sk_piece<NBUF, NOWAIT, LSUM>(r, item, s0, s1, mode, smem);
   }
 }
 
@@ -1213,7 +1273,7 @@ struct HupdSmem {
 template <int K, int GSV = 32>
 __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int maxiter, int stop_rule, int n,
                                              long n_pad, const double* __restrict__ Gpart, long g_ld, long g_split,
-                                             int nsplit, const double* __restrict__ SWpart, long sw_total,
+                                             int gsplit, int nsplit, const double* __restrict__ SWpart, long sw_total,
                                              double* __restrict__ H, double* __restrict__ SH,
                                              int* __restrict__ stop_iter, int* __restrict__ stop_reason,
                                              int* __restrict__ unchanged, int* __restrict__ classes, long cls_ld,
@@ -1247,17 +1307,17 @@ __device__ __forceinline__ void hupdate_body(const RestartInfo me, int iter, int
   };
   auto sum_g = [&](int j, double* gs) {   // chunk partials of this sample, added in chunk order
     const double* gsrc = Gpart + (long)c0 * g_ld + j;
-    for (int g0 = 0; g0 < nsplit; g0 += GS) {
+    for (int g0 = 0; g0 < gsplit; g0 += GS) {
       double v[GS][K];
 #pragma unroll
       for (int u = 0; u < GS; ++u) {   // chunks past the end re-read the last one (not added)
-        const double* q = gsrc + (long)min(g0 + u, nsplit - 1) * g_split;
+        const double* q = gsrc + (long)min(g0 + u, gsplit - 1) * g_split;
 #pragma unroll
         for (int a = 0; a < K; ++a) v[u][a] = q[(long)a * g_ld];
       }
 #pragma unroll
       for (int u = 0; u < GS; ++u)
-        if (g0 + u < nsplit) {
+        if (g0 + u < gsplit) {
 #pragma unroll
           for (int a = 0; a < K; ++a) gs[a] = (g0 + u == 0) ? v[u][a] : gs[a] + v[u][a];
         }
@@ -1421,7 +1481,8 @@ template <int GSV = 32, int MINW = 4>
 static __global__ __launch_bounds__(NTH, MINW) void k_hupdate(int iter, int maxiter, int stop_rule,
                                                         const RestartInfo* __restrict__ ri, int n, long n_pad,
                                                         const double* __restrict__ Gpart, long g_ld, long g_split,
-                                                        int nsplit, const double* __restrict__ SWpart, long sw_total,
+                                                        int gsplit, int nsplit, const double* __restrict__ SWpart,
+                                                        long sw_total,
                                                         double* __restrict__ H, double* __restrict__ SH,
                                                         int* __restrict__ stop_iter, int* __restrict__ stop_reason,
                                                         int* __restrict__ unchanged, int* __restrict__ classes,
@@ -1433,7 +1494,7 @@ static __global__ __launch_bounds__(NTH, MINW) void k_hupdate(int iter, int maxi
   if (stop_iter[me.rid] != 0) return;
 #define NMFC_HUPD_CASE(KK)                                                                                      \
   case KK:                                                                                                     \
-    hupdate_body<KK, GSV>(me, iter, maxiter, stop_rule, n, n_pad, Gpart, g_ld, g_split, nsplit, SWpart, sw_total, H, SH, \
+    hupdate_body<KK, GSV>(me, iter, maxiter, stop_rule, n, n_pad, Gpart, g_ld, g_split, gsplit, nsplit, SWpart, sw_total, H, SH, \
                      stop_iter, stop_reason, unchanged, classes, cls_ld, n_stopped, SHP, colact, Hstat, sm);   \
     break;
   switch (me.k) {

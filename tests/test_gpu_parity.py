@@ -304,8 +304,8 @@ def test_tile_shapes_bit_identical(oracle, n):
     assert relfro(ref.W[3], Wo) < TOL and relfro(ref.H[3], Ho) < TOL
 
 
-@pytest.mark.parametrize("m,R", [(4200, 160), (2000, 310)])
-def test_wta_stream_k_bit_identical(oracle, m, R):
+@pytest.mark.parametrize("m,R,lastsum", [(4200, 160, "0"), (2000, 310, "0"), (4200, 160, "1")])
+def test_wta_stream_k_bit_identical(oracle, m, R, lastsum):
     """The big W^T A tile in its stream-K form (k_wta2_sk: whole rounds of items, then the rest split at stage boundaries
     over every CU with the MFMA chains handed over) gives the bits of the one-item-per-workgroup kernel: W and H after
     fixed iterations equal bit for bit with NMFC_WTA_SK=0.  m = 4200: three gene chunks, the last 128 genes long;
@@ -321,11 +321,13 @@ def test_wta_stream_k_bit_identical(oracle, m, R):
         os.environ["NMFC_WTA_TILE"] = "big"
         for sk in ("1", "0"):
             os.environ["NMFC_WTA_SK"] = sk
+            os.environ["NMFC_WTA_LASTSUM"] = lastsum if sk == "1" else "0"   # the split-K combine probe arm (round 6)
             with Engine(A) as eng:
                 runs[sk] = eng.run(ks, R, maxiter=T, seed=9, stop_rule=0, want_factors=True, want_counts=False)
     finally:
         os.environ.pop("NMFC_WTA_TILE", None)
         os.environ.pop("NMFC_WTA_SK", None)
+        os.environ.pop("NMFC_WTA_LASTSUM", None)
     a, b = runs["1"], runs["0"]
     for j in range(len(ks) * R):
         assert np.array_equal(a.W[j], b.W[j]) and np.array_equal(a.H[j], b.H[j]), j

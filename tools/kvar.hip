@@ -576,10 +576,10 @@ int main(int argc, char** argv) {
     CK(hipMemset(flg, 0, sizeof(unsigned) * ncu));
     const long sk_stages = (long)ng * ntj * ((m_pad + 15) / 16);
     const int gsk = (int)std::min<long>(ncu, sk_stages / (kchunk / 16));
-    auto SK = [&](int G, bool nowait) {
+    auto SK = [&](int G, bool nowait, int dpx = 0) {
       ++epoch;
       const SkArgs a{W, Ablk, m_pad, ng, ntj, kchunk, dprb, dpre, dri, dci, stop, Gpart, g_ld, g_split, SWpart, (long)sq,
-                     fixb, flg, epoch, nsplit};
+                     fixb, flg, epoch, nsplit, nullptr, dpx};
       if (nowait)
         hipLaunchKernelGGL((k_wta2_sk<3, true>), dim3(G), dim3(SK_THREADS), 0, 0, a);
       else
@@ -598,9 +598,10 @@ int main(int argc, char** argv) {
       };
       grab(g1, s1, [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); });
       for (int G : {gsk, gsk / 2 + 1, 37}) {
-        for (int nw = 0; nw < 2; ++nw) {
-          grab(g2, s2, [&] { SK(G, nw == 1); });
-          printf("  stream-K G=%d%s vs engine big tile: G partials %s, Gram partials %s\n", G, nw ? " (recompute path)" : "",
+        for (int nw = 0; nw < 3; ++nw) {
+          grab(g2, s2, [&] { SK(G, nw == 1, nw == 2); });
+          printf("  stream-K G=%d%s vs engine big tile: G partials %s, Gram partials %s\n", G,
+                 nw == 1 ? " (recompute path)" : nw == 2 ? " (XCD-contiguous rounds)" : "",
                  memcmp(g1.data(), g2.data(), sizeof(double) * gn) ? "DIFFER" : "bit-identical",
                  memcmp(s1.data(), s2.data(), sizeof(double) * sn) ? "DIFFER" : "bit-identical");
         }
@@ -612,6 +613,7 @@ int main(int argc, char** argv) {
           {"k_wta2 big 4x128 nbuf3 GREG (8 waves)", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, true, false, true); }},
           {"  16 waves, GREG (engine)", [&] { WAT(1024, 4, 128, 4, 4, 1, 3, 1, true, true, false, true); }},
           {"  stream-K 16 waves GREG, G = CUs", [&] { SK(gsk, false); }},
+          {"  stream-K, XCD-contiguous whole rounds", [&] { SK(gsk, false, 1); }},
           {"  stream-K, recompute path (no hand-off)", [&] { SK(gsk, true); }},
           {"  Gram in LDS chains (round 3 form)", [&] { WA(4, 128, 4, 2, 1, 3, 1, true); }},
           {"  no Gram chains", [&] { WA(4, 128, 4, 2, 1, 3, 1, true, false); }},

@@ -277,7 +277,7 @@ int main(int argc, char** argv) {
     }
     report("hupdate", timeit([&] {
              hipLaunchKernelGGL(k_hupdate<>, dim3(nlive), dim3(NTH), 0, 0, 1, 1000000, STOP_FIXED, dri, n, n_pad, Gpart,
-                                g_ld, g_split, nsplit, SWpart, sw_total, Hh, SH, stop, reason, unch, cls, (long)512, nst,
+                                g_ld, g_split, nsplit, nsplit, SWpart, sw_total, Hh, SH, stop, reason, unch, cls, (long)512, nst,
                                 SHP, colact, Hstat);
            }, reps));
     CK(hipMemcpy(colact, ca.data(), sizeof(int) * ca.size(), hipMemcpyHostToDevice));   // hupdate stamped iter 1
