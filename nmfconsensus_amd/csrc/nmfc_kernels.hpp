@@ -1062,18 +1062,17 @@ static __global__ __launch_bounds__(SK_THREADS, 1) void k_wta2_sk(SkArgs args) {
   const int t0 = tail ? 1 : 0;
   const int npieces = t0 + ndp + nfull + (head ? 1 : 0);
   for (int pc = 0; pc < npieces; ++pc) {
-    // piece order: the start piece first (a later range waits for it), the whole rounds, the split part's whole items,
-    // the continuation last
+    // piece order: the whole rounds first -- every workgroup starts them together, so the workgroups that share an A
+    // or W stage read it at the same time and L2 serves all but the first (starting with the split part's start pieces,
+    // of every length, desynchronised them and tripled the L2-miss bytes) -- then the split part: the start piece (a
+    // later range waits for it), its whole items, the continuation last.  With shares of at least one item the start
+    // piece of range r - 1 ends before range r reaches its continuation, so nobody waits.
     int item, s0, s1, mode;
-    if (pc < t0) {
-      item = ie, s0 = 0, s1 = se, mode = 1;
-    } else if (pc < t0 + ndp) {
-      // whole rounds: round k is items k G .. k G + G - 1 (k_wta2's first rounds), workgroup r taking k G + r; or
-      // (dp_xcd) XCD-contiguous: the xc workgroups of an XCD walk the XCD's own block of ndp x xc items together, so an
-      // XCD stays on one chunk's A and neighbouring panel groups' W rows over several rounds -- bit-identical either
-      // way, a speed / L2-residency probe
-      item = A->dp_xcd ? ndp * xb + (pc - t0) * xc + (r - xb) : (pc - t0) * G + r;
+    if (pc < ndp) {
+      item = A->dp_xcd ? ndp * xb + pc * xc + (r - xb) : pc * G + r;
       s0 = 0, s1 = nst_of(item), mode = 0;
+    } else if (pc < ndp + t0) {
+      item = ie, s0 = 0, s1 = se, mode = 1;
     } else if (head && pc == npieces - 1) {
       item = ib, s0 = sb, s1 = nst_of(ib), mode = 2;
     } else {

@@ -14,13 +14,14 @@ root, reps = sys.argv[1], int(sys.argv[2])
 
 def rows(sub):
     out = collections.defaultdict(lambda: collections.defaultdict(float))
-    names = {}
+    names, dur = {}, {}
     for f in glob.glob(os.path.join(root, sub, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             d = int(r["Dispatch_Id"])
             names[d] = r["Kernel_Name"]
             out[d][r["Counter_Name"]] += float(r["Counter_Value"])
-    return out, names
+            dur[d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    return out, names, dur
 
 
 def label(name):
@@ -31,14 +32,14 @@ def label(name):
     return None
 
 
-fetch, names = rows("FETCH_SIZE")
-write, _ = rows("WRITE_SIZE")
+fetch, names, dur = rows("FETCH_SIZE")
+write, _, _ = rows("WRITE_SIZE")
 groups = collections.defaultdict(list)
 for d in sorted(fetch):
     lb = label(names[d])
     if lb:
         groups[lb].append(d)
-print(f"{'arm':34s} {'launches':>8s} {'GB/launch':>10s} {'Mcycles':>8s}   (GHz = Mcycles / the arm's kvar ms / 1000)")
+print(f"{'arm':34s} {'launches':>8s} {'GB/launch':>10s} {'Mcycles':>8s} {'ms(pmc)':>8s} {'GHz':>6s}   (cycles: GRBM_GUI_ACTIVE / 8)")
 for lb, ds in groups.items():
     parts = [(lb, ds)]
     if lb == "k_wta2_sk" and len(ds) >= 2 * reps:   # round-robin arm first, then the XCD-contiguous arm
@@ -46,4 +47,5 @@ for lb, ds in groups.items():
     for nm, dd in parts:
         gb = sum(fetch[d].get("FETCH_SIZE", 0) * 2 * 1024 + write[d].get("WRITE_SIZE", 0) * 1024 for d in dd) / len(dd) / 1e9
         cyc = sum(fetch[d].get("GRBM_GUI_ACTIVE", 0) / 8 for d in dd) / len(dd)
-        print(f"{nm:34s} {len(dd):8d} {gb:10.3f} {cyc / 1e6:8.3f}")
+        t = sum(dur[d] for d in dd) / len(dd)
+        print(f"{nm:34s} {len(dd):8d} {gb:10.3f} {cyc / 1e6:8.3f} {t * 1e3:8.3f} {cyc / t / 1e9:6.3f}")
