@@ -725,7 +725,7 @@ def side_kernels(A_dev, m, n, k, reps=3):
     return out
 
 
-PMC_NAMES = {"wta": ("k_wta2", "k_wta_narrow", "k_wta_narrow_lc"), "ahtw": ("k_ahtw4",), "hupdate": ("k_hupdate",),
+PMC_NAMES = {"wta": ("k_wta2", "k_wta2_sk", "k_wta_narrow", "k_wta_narrow_lc"), "ahtw": ("k_ahtw4",), "hupdate": ("k_hupdate",),
              "labels": ("k_labels",), "counts": ("k_counts",)}
 
 
