@@ -305,6 +305,7 @@ struct nmfc_engine {
   DevBuf solojobs;                  // batched k_solo_mu jobs (small shapes, rank <= 4)
   bool narrow_lc = true;            // env NMFC_NARROW_LC=0: the one-wave narrow W^T A kernel
   bool wta_sk = true;               // env NMFC_WTA_SK=0: the big W^T A tile one item per workgroup (no stream-K)
+  bool wta_sk_mid = true;           // env NMFC_WTA_SK_MID=0: the same for the 2-panel tile
   bool wta_lastsum = false;         // env NMFC_WTA_LASTSUM=1: k_wta2_sk sums each tile's chunk partials (probe arm)
   int sk_dp_xcd = 0;                // env NMFC_SK_DP_XCD=1: k_wta2_sk's whole rounds in XCD-contiguous blocks (probe)
   DevBuf skfix, skflag, sktcnt;     // k_wta2_sk: per-range hand-off slots and flags (zeroed once), per-tile tickets
@@ -363,9 +364,11 @@ struct TileChoice {
 // C3 full-load grid of 6.72 rounds, i.e. ~1 % above the ideal 6.72 / 7 of the unsplit form's time)
 constexpr double WTA_SK_COST = 1.01;
 bool sk_big_ok(const nmfc_engine* e, int ntj) { return e->wta_sk && WTA_W16 && ntj >= 4; }
-// ... and its grid condition: at least one whole round of items, and every workgroup's even share of the stages at least
-// one item long (so an item is cut into at most two pieces: k_wta2_sk's contract)
-bool sk_big_fits(const nmfc_engine* e, long ngroups, int ntj) {
+// the 2-panel tile's stream-K form (k_wta2_sk<..., 2>): its 8-wave register-Gram instantiation (ntj >= 4)
+bool sk_mid_ok(const nmfc_engine* e, int ntj) { return e->wta_sk && e->wta_sk_mid && WTA_MID_GREG && ntj >= 4; }
+// ... and the grid condition of either: at least one whole round of items, and every workgroup's even share of the
+// stages at least one item long (so an item is cut into at most two pieces: k_wta2_sk's contract)
+bool sk_grid_fits(const nmfc_engine* e, long ngroups, int ntj) {
   const long ipc = ngroups * ntj, nitems = ipc * e->nsplit;
   const long nst_full = e->kchunk / 16, nst_last = (e->m_pad - (long)(e->nsplit - 1) * e->kchunk) / 16;
   const long nst_max = e->nsplit > 1 ? nst_full : nst_last;
@@ -385,17 +388,18 @@ TileChoice choose_tiles(const nmfc_engine* e, int np_live, int ntj) {
     double wgs;
     long slots;
     double t;
-  } cands[4] = {{0, (double)(ns * ((np + 3) / 4) * ntj), cu, 2.0 * WTA_SK_COST},
+  } cands[4] = {{0, (double)(ns * ((np + 3) / 4) * ntj), cu, 2.0},
                 {3, (double)(ns * ((np + 1) / 2) * ntj), cu, 1.0},
                 {1, (double)(ns * np) * (2 * ntj + (e->gram_model ? 0.75 : 0.0)), 3 * cu, 0.8},
                 {2, (double)(ns * np) * (4 * ntj + (e->gram_model ? 1.5 : 0.0)), 4 * cu, 0.6}};
   TileChoice tc{0, false};
   double best = 1e300;
   for (const Cand& c : cands) {
-    // the big tile in its stream-K form (k_wta2_sk, from one whole round of items on) takes wgs / slots rounds, not
-    // ceil(wgs / slots): the last round's items are split over every CU
-    const bool sk = c.id == 0 && sk_big_ok(e, ntj) && sk_big_fits(e, (np + 3) / 4, ntj);
-    const double est = (sk ? c.wgs / (double)c.slots : std::ceil(c.wgs / (double)c.slots)) * c.t;
+    // the big and 2-panel tiles in their stream-K form (k_wta2_sk, from one whole round of items on) take wgs / slots
+    // rounds, not ceil(wgs / slots): the last round's items are split over every CU
+    const bool sk = (c.id == 0 && sk_big_ok(e, ntj) && sk_grid_fits(e, (np + 3) / 4, ntj)) ||
+                    (c.id == 3 && sk_mid_ok(e, ntj) && sk_grid_fits(e, (np + 1) / 2, ntj));
+    const double est = sk ? c.wgs / (double)c.slots * c.t * WTA_SK_COST : std::ceil(c.wgs / (double)c.slots) * c.t;
     if (est < best - 1e-9) {
       best = est;
       tc.wta = c.id;
@@ -635,6 +639,7 @@ nmfc_engine* nmfc_engine_create(int device, const double* A, int m, int n, int a
   if (const char* s = getenv("NMFC_SOLO")) e->solo_ok = atoi(s) != 0;
   if (const char* s = getenv("NMFC_NARROW_LC")) e->narrow_lc = atoi(s) != 0;
   if (const char* s = getenv("NMFC_WTA_SK")) e->wta_sk = atoi(s) != 0;
+  if (const char* s = getenv("NMFC_WTA_SK_MID")) e->wta_sk_mid = atoi(s) != 0;
   if (const char* s = getenv("NMFC_WTA_LASTSUM")) e->wta_lastsum = atoi(s) != 0;
   if (const char* s = getenv("NMFC_SK_DP_XCD")) e->sk_dp_xcd = atoi(s) != 0;
   if (const char* s = getenv("NMFC_GRAM_MODEL")) e->gram_model = atoi(s) != 0;
@@ -1122,24 +1127,29 @@ int nmfc_engine_run(nmfc_engine* e, const int* ks, int nk, int R, const nmfc_swe
                                  e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ntq, e->nsplit, e->kchunk, nblk,
                                  e->colinfo.as<ColInfo>(),
                                  e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total);
-          } else if (wta_big && sk_big_ok(e, ntj) && sk_big_fits(e, pk.npanels / WTA_NPT, ntj)) {
+          } else if ((wta_big && sk_big_ok(e, ntj) && sk_grid_fits(e, pk.npanels / WTA_NPT, ntj)) ||
+                     (wta_mid && sk_mid_ok(e, ntj) && sk_grid_fits(e, (lp + 1) / 2, ntj))) {
             // stream-K form: ncu persistent workgroups, whole rounds of items then the rest split evenly (bit-identical
             // to the one-item-per-workgroup tile: the same MFMA chains, handed over at a stage boundary)
             if (!e->skflag.p) {
               if (e->skfix.ensure(sizeof(double) * SK_FIX * e->ncu) || e->skflag.ensure(sizeof(unsigned) * e->ncu)) return -1;
               HCHECK(hipMemsetAsync(e->skflag.p, 0, sizeof(unsigned) * e->ncu, st));
             }
-            const long tiles = (long)(pk.npanels / WTA_NPT) * ntj;
-            if (e->wta_lastsum && e->sktcnt.bytes < sizeof(unsigned) * tiles) {
+            const int ng = wta_big ? pk.npanels / WTA_NPT : (lp + 1) / 2;
+            const long tiles = (long)ng * ntj;
+            const bool lastsum = e->wta_lastsum && wta_big;
+            if (lastsum && e->sktcnt.bytes < sizeof(unsigned) * tiles) {
               if (e->sktcnt.ensure(sizeof(unsigned) * tiles)) return -1;   // fresh tickets: zero
               HCHECK(hipMemsetAsync(e->sktcnt.p, 0, sizeof(unsigned) * tiles, st));
             }
-            const SkArgs a{e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, pk.npanels / WTA_NPT, ntj, e->kchunk,
+            const SkArgs a{e->W[cur].as<double>(), e->Ablk.as<double>(), e->m_pad, ng, ntj, e->kchunk,
                            e->prb.as<int>(), e->pre.as<int>(), e->rinfo.as<RestartInfo>(), e->colinfo.as<ColInfo>(),
                            e->stop_iter.as<int>(), e->Gpart.as<double>(), g_ld, g_split, e->SWpart.as<double>(), sw_total,
                            e->skfix.as<double>(), e->skflag.as<unsigned>(), ++e->sk_epoch, e->nsplit,
                            e->sktcnt.as<unsigned>(), e->sk_dp_xcd};
-            if (e->wta_lastsum) {
+            if (!wta_big) {
+              hipLaunchKernelGGL((k_wta2_sk<WTA_MID_NBUF, false, false, 2>), dim3(e->ncu), dim3(SK_THREADS / 2), 0, st, a);
+            } else if (lastsum) {
               hipLaunchKernelGGL((k_wta2_sk<GT_NBUF, false, true>), dim3(e->ncu), dim3(SK_THREADS), 0, st, a);
               gsplit = 1;   // every tile's chunk partials summed into chunk slot 0
             } else {

@@ -730,8 +730,8 @@ static __global__ __launch_bounds__(WR * WC * 64, MINW) void k_wta2(const double
 // this launch); reader lane 0 relaxed agent poll -> agent acquire fence -> vmcnt(0) -> barrier -> plain loads.
 // fix: G slots of SK_FIX doubles (9 d4 per lane: the 8 accumulator blocks and the Gram chain); flags: G words.
 // ---------------------------------------------------------------------------------------------
-constexpr int SK_THREADS = 1024;
-constexpr long SK_FIX = 9L * 4 * SK_THREADS;   // doubles per range slot
+constexpr int SK_THREADS = 1024;              // the 4-panel tile's 16 waves (the 2-panel tile: 8, SK_THREADS / 2)
+constexpr long SK_FIX = 9L * 4 * SK_THREADS;   // doubles per range slot (either tile: 8 blocks + the Gram chain per lane)
 constexpr int SK_POLLS = 256;                  // x s_sleep 127 (~3.4 us each): ~0.9 ms before recomputing
 
 // A wave-uniform copy of a value held in VGPRs (device-function arguments arrive in VGPRs): SGPR operands for the
@@ -793,11 +793,14 @@ __device__ __forceinline__ SkArgsK sk_args() {
 // the tile's nsplit partials in chunk order -- k_hupdate's order, the same bits -- into chunk slot 0, so k_hupdate
 // reads one partial instead of nsplit.  Publication: every wave vmcnt(0) -> barrier -> lane 0 agent release -> ticket;
 // the ticket that completes the tile -> agent acquire -> barrier -> plain loads.
-template <int NBUF, bool NOWAIT, bool LSUM = false>
+// NPT: 4 (the 16-wave big tile) or 2 (the 8-wave 2-panel tile of k_wta2<2, 128, 2, 4, ...>: wave rows = panels, the same
+// register Gram scheme, one workgroup per CU; round 6, for grids between one and two rounds of it -- the 8-GPU shard).
+template <int NBUF, bool NOWAIT, bool LSUM = false, int NPT = 4>
 __device__ __forceinline__ void wta_sk_piece(int r, int item_in, int s0_in, int s1_in, int mode_in,
                                              char* __restrict__ smem) {
-  constexpr int NPT = 4, RQ = 128, WC = 4;
-  using T = GTile<64 * NPT, RQ, 4, WC, NBUF, true, true, true, true>;
+  constexpr int RQ = 128, WC = 4;
+  using T = GTile<64 * NPT, RQ, NPT, WC, NBUF, true, true, true, true>;
+  static_assert(T::MB * T::NB == 8 && T::NTH <= SK_THREADS, "a slot holds 8 accumulator blocks + the Gram chain per lane");
   SkArgsK A = sk_args();
   const double* W = A->W;
   const double* Acm = A->Acm;
@@ -819,7 +822,7 @@ __device__ __forceinline__ void wta_sk_piece(int r, int item_in, int s0_in, int 
     return v;
   };
   int* need = reinterpret_cast<int*>(smem + T::LDS_BYTES);   // 28 Gram candidates
-  int* okw = need + 28;                                       // the continuation's "published" word
+  int* okw = need + 7 * NPT;                                  // the continuation's "published" word
   const int w = wave_id();
   const int t = uni(item % ntj);
   const int pg = uni((item / ntj) % ngroups);
@@ -877,7 +880,7 @@ __device__ __forceinline__ void wta_sk_piece(int r, int item_in, int s0_in, int 
 #pragma unroll
         for (int nb = 0; nb < T::NB; ++nb)
           tl.acc[mb][nb] = *reinterpret_cast<const d4*>(src + ((long)(mb * T::NB + nb) * SK_THREADS + ln) * 4);
-      tl.gacc = *reinterpret_cast<const d4*>(src + (8L * SK_THREADS + ln) * 4);
+      tl.gacc = *reinterpret_cast<const d4*>(src + ((long)T::MB * T::NB * SK_THREADS + ln) * 4);
     }
     return true;
   };
@@ -924,7 +927,7 @@ __device__ __forceinline__ void wta_sk_piece(int r, int item_in, int s0_in, int 
 #pragma unroll
       for (int nb = 0; nb < T::NB; ++nb)
         *reinterpret_cast<d4*>(dst + ((long)(mb * T::NB + nb) * SK_THREADS + ln) * 4) = tl.acc[mb][nb];
-    *reinterpret_cast<d4*>(dst + (8L * SK_THREADS + ln) * 4) = tl.gacc;
+    *reinterpret_cast<d4*>(dst + ((long)T::MB * T::NB * SK_THREADS + ln) * 4) = tl.gacc;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (w == 0 && ln == 0) {
@@ -1012,10 +1015,10 @@ __device__ __forceinline__ void wta_sk_piece(int r, int item_in, int s0_in, int 
 }
 
 // NOWAIT (tools/kvar.hip only): every continuation takes the recompute path (tests its bits)
-template <int NBUF = GT_NBUF, bool NOWAIT = false, bool LSUM = false>
-static __global__ __launch_bounds__(SK_THREADS, 1) void k_wta2_sk(SkArgs args) {
-  using T = GTile<256, 128, 4, 4, NBUF, true, true, true, true>;
-  static_assert(T::NTH == SK_THREADS, "16 waves");
+template <int NBUF = GT_NBUF, bool NOWAIT = false, bool LSUM = false, int NPT = 4>
+static __global__ __launch_bounds__(64 * NPT * 4, 1) void k_wta2_sk(SkArgs args) {
+  using T = GTile<64 * NPT, 128, NPT, 4, NBUF, true, true, true, true>;
+  static_assert(NPT == 4 || NPT == 2, "the 16-wave 4-panel tile or the 8-wave 2-panel tile");
   __shared__ __attribute__((aligned(1024))) char smem[T::LDS_BYTES + 128];
   (void)args;   // read through sk_args() (the kernarg segment), see there
   SkArgsK A = sk_args();
@@ -1079,7 +1082,7 @@ static __global__ __launch_bounds__(SK_THREADS, 1) void k_wta2_sk(SkArgs args) {
       item = f0 + pc - t0 - ndp, s0 = 0, s1 = nst_of(item), mode = 0;
     }
     __syncthreads();   // the previous piece's LDS ring, need[] and okw are free
-    wta_sk_piece<NBUF, NOWAIT, LSUM>(r, item, s0, s1, mode, smem);
+    wta_sk_piece<NBUF, NOWAIT, LSUM, NPT>(r, item, s0, s1, mode, smem);
   }
 }
 

