@@ -145,24 +145,27 @@ __device__ __forceinline__ double quot(double a, double p) {
 #endif
 }
 
-// elements per lane: the LDS return path moves 8K bytes per lane for every element-restart's operand
-// row; where that (rather than the VALU work) bounds the kernel, each row serves 2 elements.  Measured
-// per k (tools/brunet_kbench.py, profiles/r01f_brunet_spl.txt): a gain for k = 8, 9 only -- elsewhere the
-// doubled register state costs more occupancy than the LDS traffic saves.
-constexpr int spl_of(int K) { return ((NMFC_BR_SPL_MASK >> K) & 1) ? 2 : 1; }
-// restarts per workgroup: each lane keeps SPL * RG * 4K VGPRs of state (operand rows in, accumulators
-// out); RG shares every A element loaded over RG restarts.  Per-k values measured on the C5 shape
-// (profiles/r01g/brunet_rg/): the best RG is not monotone in k because register-count occupancy
-// steps and grid size (groups = R / RG) move together; RG never changes a restart's arithmetic.
-constexpr int rg_of(int K) {
-  return spl_of(K) == 2 ? (K <= 6 ? 2 : 1)
-                        : (K <= 2 ? NMFC_BR_RG2 : K <= 3 ? NMFC_BR_RG3 : K <= 4 ? NMFC_BR_RG4 : K <= 5 ? NMFC_BR_RG5
-                           : K <= 6 ? NMFC_BR_RG6 : K <= 7 ? NMFC_BR_RG7 : K <= 10 ? NMFC_BR_RG10 : 1);
-}
+// Per-rank configuration of the two VALU kernels (tables in nmfc_tuning.hpp, per kernel since round 6):
+//  SPL  elements per lane: the LDS return path moves 8K bytes per lane for every element-restart's operand row; where
+//       that (rather than the VALU work) bounds the kernel, each row serves 2 elements (k = 8, 9; elsewhere the doubled
+//       register state costs more occupancy than the traffic saves: profiles/r01f_brunet_spl.txt).
+//  RG   restarts per workgroup: each lane keeps SPL * RG * 4K values of state; RG shares every A element loaded over RG
+//       restarts.  The best RG is not monotone in k: register-count occupancy steps and grid size (groups = R / RG)
+//       move together (profiles/r01g/brunet_rg/, profiles/r06/brunet_sload/).  RG never changes a restart's arithmetic.
+//  SL   the wave-uniform operand rows by scalar loads into SGPR operands instead of the double-buffered LDS tiles: no
+//       LDS return-path bytes and no barriers, and the rows leave the VGPRs (occupancy up a step for k >= 4); the same
+//       arithmetic in the same order, so the same bits.
+constexpr int br_nib(unsigned long long t, int K) { return K < 16 ? (int)((t >> (4 * K)) & 15) : 0; }
+constexpr int rgh_of(int K) { return br_nib(NMFC_BR_RGH, K) ? br_nib(NMFC_BR_RGH, K) : 1; }
+constexpr int rgw_of(int K) { return br_nib(NMFC_BR_RGW, K) ? br_nib(NMFC_BR_RGW, K) : 1; }
+constexpr int splh_of(int K) { return ((NMFC_BR_SPLH >> K) & 1ULL) ? 2 : 1; }
+constexpr int splw_of(int K) { return ((NMFC_BR_SPLW >> K) & 1ULL) ? 2 : 1; }
+constexpr bool slh_of(int K) { return (NMFC_BR_SLH >> K) & 1ULL; }
+constexpr bool slw_of(int K) { return (NMFC_BR_SLW >> K) & 1ULL; }
 // small batches (B <= NMFC_BR_SMALL_B restarts of one k, e.g. one rank's shard of a strong-scaling
 // run): fewer restarts per workgroup so the batch still spreads over the CUs
-constexpr int rg_small(int K) {
-  return NMFC_BR_RG_SMALL_DIV == 0 ? 1 : (rg_of(K) / NMFC_BR_RG_SMALL_DIV > 1 ? rg_of(K) / NMFC_BR_RG_SMALL_DIV : 1);
+constexpr int rg_small(int rg) {
+  return NMFC_BR_RG_SMALL_DIV == 0 ? 1 : (rg / NMFC_BR_RG_SMALL_DIV > 1 ? rg / NMFC_BR_RG_SMALL_DIV : 1);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -242,7 +245,7 @@ struct OperandTiles {
 // VP[i][j] = sum_c W[b][i][c] H[b][j][c].  Lane = SPL samples j (H columns and accumulators in
 // registers); W rows through the double-buffered LDS tiles.  A broadcast ds_read_b128 still moves
 // 1 KiB per wave through the LDS return path, so for larger k each W row read serves SPL = 2 samples.
-template <int K, int RG, int SPL>
+template <int K, int RG, int SPL, bool SL>
 __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, long n_pad, int m, int n, int gc,
                                                 const int* __restrict__ act, int nact, const double* __restrict__ W,
                                                 long wstride, const double* __restrict__ H, long hstride,
@@ -262,6 +265,9 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
   const int i0 = chunk * gc, i1 = min(m, i0 + gc);
   if (threadIdx.x < RG) sl[threadIdx.x] = act[min(g0 + (int)threadIdx.x, nact - 1)];
   __syncthreads();
+  long wro[RG];   // SL: each restart's W row base, wave-uniform
+#pragma unroll
+  for (int r = 0; r < RG; ++r) wro[r] = (long)__builtin_amdgcn_readfirstlane(sl[r]) * wstride;
   double h[SPL][RG][K], g[SPL][RG][K];
 #pragma unroll
   for (int s = 0; s < SPL; ++s)
@@ -273,15 +279,18 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
         g[s][r][c] = 0.0;
       }
   OT ot;
-  ot.fetch(W, wstride, sl, i0, i1);
-  ot.store(wl[0]);
-  __syncthreads();
+  if constexpr (!SL) {
+    ot.fetch(W, wstride, sl, i0, i1);
+    ot.store(wl[0]);
+    __syncthreads();
+  }
   int buf = 0;
   for (int t0 = i0; t0 < i1; t0 += TL, buf ^= 1) {
-    const bool more = t0 + TL < i1;
+    const bool more = !SL && t0 + TL < i1;
     if (more) ot.fetch(W, wstride, sl, t0 + TL, i1);
     const double* ap = Arm + (long)t0 * n_pad;
     const double* wt = wl[buf];
+    const double* wg = W + (long)t0 * K;
     // slots past the live restarts repeat the last live one (computed, never stored): no branches here
     auto gene = [&](int ii) {
       double a[SPL];
@@ -289,7 +298,7 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
       for (int s = 0; s < SPL; ++s) a[s] = ap[(long)ii * n_pad + jl[s]];
 #pragma unroll
       for (int r = 0; r < RG; ++r) {
-        const double* wr = wt + r * (TL * K) + ii * K;
+        const double* wr = SL ? wg + wro[r] + ii * K : wt + r * (TL * K) + ii * K;
         double w[K];
 #pragma unroll
         for (int c = 0; c < K; ++c) w[c] = wr[c];
@@ -310,8 +319,10 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
     } else {
       for (int ii = 0; ii < i1 - t0; ++ii) gene(ii);
     }
-    if (more) ot.store(wl[buf ^ 1]);
-    __syncthreads();
+    if constexpr (!SL) {
+      if (more) ot.store(wl[buf ^ 1]);
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int s = 0; s < SPL; ++s)
@@ -439,7 +450,7 @@ __global__ __launch_bounds__(BT) void k_br_hupd(int t, int check, int stopconv, 
 
 // W side: lane = SPL genes i over every sample j: F[i][c] = sum_j A[i][j] / VP[i][j] * H[j][c] with the
 // new H (LDS tiles of TL samples) and the old W rows in registers; W <- (W * F + eps) / rowSums(H).
-template <int K, int RG, int SPL>
+template <int K, int RG, int SPL, bool SL>
 __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, long m_pad, int m, int n,
                                                 const int* __restrict__ act, int nact, double* __restrict__ W,
                                                 long wstride, const double* __restrict__ H, long hstride,
@@ -457,6 +468,9 @@ __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, 
   const int nlive = min(RG, nact - g0);
   if (threadIdx.x < RG) sl[threadIdx.x] = act[min(g0 + (int)threadIdx.x, nact - 1)];
   __syncthreads();
+  long hro[RG];   // SL: each restart's H row base, wave-uniform
+#pragma unroll
+  for (int r = 0; r < RG; ++r) hro[r] = (long)__builtin_amdgcn_readfirstlane(sl[r]) * hstride;
   double w[SPL][RG][K], f[SPL][RG][K];
 #pragma unroll
   for (int s = 0; s < SPL; ++s)
@@ -468,22 +482,25 @@ __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, 
         f[s][r][c] = 0.0;
       }
   OT ot;
-  ot.fetch(H, hstride, sl, 0, n);
-  ot.store(hl[0]);
-  __syncthreads();
+  if constexpr (!SL) {
+    ot.fetch(H, hstride, sl, 0, n);
+    ot.store(hl[0]);
+    __syncthreads();
+  }
   int buf = 0;
   for (int s0 = 0; s0 < n; s0 += TL, buf ^= 1) {
-    const bool more = s0 + TL < n;
+    const bool more = !SL && s0 + TL < n;
     if (more) ot.fetch(H, hstride, sl, s0 + TL, n);
     const double* ap = Acm + (long)s0 * m_pad;
     const double* ht = hl[buf];
+    const double* hg = H + (long)s0 * K;
     auto sample = [&](int jj) {
       double a[SPL];
 #pragma unroll
       for (int s = 0; s < SPL; ++s) a[s] = ap[(long)jj * m_pad + il[s]];
 #pragma unroll
       for (int r = 0; r < RG; ++r) {
-        const double* hj = ht + r * (TL * K) + jj * K;
+        const double* hj = SL ? hg + hro[r] + jj * K : ht + r * (TL * K) + jj * K;
         double hh[K];
 #pragma unroll
         for (int c = 0; c < K; ++c) hh[c] = hj[c];
@@ -504,8 +521,10 @@ __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, 
     } else {
       for (int jj = 0; jj < n - s0; ++jj) sample(jj);
     }
-    if (more) ot.store(hl[buf ^ 1]);
-    __syncthreads();
+    if constexpr (!SL) {
+      if (more) ot.store(hl[buf ^ 1]);
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int s = 0; s < SPL; ++s)
@@ -658,10 +677,10 @@ struct nmfc_brunet {
 namespace {
 
 // one k: B restarts (slots 0..B-1) already initialised in L->W / L->H; iterates to the stop rule.
-template <int K, int RG = rg_of(K)>
+template <int K, int RGH = rgh_of(K), int RGW = rgw_of(K)>
 int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o, std::vector<int>& iters,
                std::vector<int>& stopped) {
-  constexpr int SPL = spl_of(K);
+  constexpr int SPLH = splh_of(K), SPLW = splw_of(K);
   const int m = e->m, n = e->n;
   hipStream_t st = L->st;
   const long wstride = (long)m * K, hstride = (long)n * K;
@@ -677,10 +696,11 @@ int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o
   const double fl = 4.0 * m * n * K;   // algorithmic flop per restart and kernel: VP (2mnk) + product (2mnk)
   for (int t = 1; t <= o.maxiter && nact > 0; ++t) {
     const int check = (t % o.stopfreq) == 0;
-    const int groups = (nact + RG - 1) / RG;
+    const int groups_h = (nact + RGH - 1) / RGH, groups_w = (nact + RGW - 1) / RGW;
     {
       BTimed tl(L, BK_HNUM, fl * nact);
-      hipLaunchKernelGGL((k_br_hnum<K, RG, SPL>), dim3((n + BT * SPL - 1) / (BT * SPL), e->nchunks, groups), dim3(BT), 0, st,
+      hipLaunchKernelGGL((k_br_hnum<K, RGH, SPLH, slh_of(K)>), dim3((n + BT * SPLH - 1) / (BT * SPLH), e->nchunks, groups_h),
+                         dim3(BT), 0, st,
                          e->Arm.as<double>(), e->n_pad, m, n, e->gc, L->act.as<int>(), nact, L->W.as<double>(), wstride,
                          L->H.as<double>(), hstride, L->Gp.as<double>(), gp_cs);
     }
@@ -692,7 +712,8 @@ int br_iterate(const nmfc_brunet* e, BrLane* L, int B, const nmfc_brunet_opts& o
     }
     {
       BTimed tl(L, BK_WUPD, fl * nact);
-      hipLaunchKernelGGL((k_br_wupd<K, RG, SPL>), dim3((m + BT * SPL - 1) / (BT * SPL), groups), dim3(BT), 0, st, e->Acm.as<double>(),
+      hipLaunchKernelGGL((k_br_wupd<K, RGW, SPLW, slw_of(K)>), dim3((m + BT * SPLW - 1) / (BT * SPLW), groups_w), dim3(BT), 0, st,
+                         e->Acm.as<double>(),
                          e->m_pad, m, n, L->act.as<int>(), nact, L->W.as<double>(), wstride, L->H.as<double>(), hstride,
                          L->RS.as<double>());
     }
@@ -730,7 +751,7 @@ int br_dispatch(const nmfc_brunet* e, BrLane* L, int K, int B, const nmfc_brunet
   switch (K) {
 #define BR_CASE(KK) \
   case KK:          \
-    return B <= NMFC_BR_SMALL_B ? br_iterate<KK, rg_small(KK)>(e, L, B, o, iters, stopped) \
+    return B <= NMFC_BR_SMALL_B ? br_iterate<KK, rg_small(rgh_of(KK)), rg_small(rgw_of(KK))>(e, L, B, o, iters, stopped) \
                                 : br_iterate<KK>(e, L, B, o, iters, stopped);
     BR_CASE(2) BR_CASE(3) BR_CASE(4) BR_CASE(5) BR_CASE(6) BR_CASE(7) BR_CASE(8) BR_CASE(9) BR_CASE(10) BR_CASE(11)
     BR_CASE(12) BR_CASE(13) BR_CASE(14) BR_CASE(15) BR_CASE(16)

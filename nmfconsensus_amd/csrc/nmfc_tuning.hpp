@@ -59,29 +59,26 @@
 #ifndef NMFC_BRUNET_IEEEDIV
 #define NMFC_BRUNET_IEEEDIV 0   // 1: the compiler's IEEE divide instead of rcp + Newton + residual correction
 #endif
-#ifndef NMFC_BR_SPL_MASK
-#define NMFC_BR_SPL_MASK ((1 << 8) | (1 << 9))   // bit k set: 2 elements per lane for rank k
+// Brunet per-rank kernel configuration, one table per kernel (H side k_br_hnum, W side k_br_wupd), nibble / bit k for
+// rank k (ranks 0..15; rank 16 and any nibble 0 mean 1 restart per workgroup, no SPL, LDS operand rows).  Measured per
+// k and kernel on the C5 shape (tools/brunet_kbench.py; profiles/r06/brunet_sload/).
+#ifndef NMFC_BR_RGH
+#define NMFC_BR_RGH 0x11121334500ULL   // restarts per workgroup (RG), H side: k = 2..10 -> 5 4 3 3 1 2 1 1 1
 #endif
-#ifndef NMFC_BR_RG2
-#define NMFC_BR_RG2 5           // restarts per workgroup, rank 2 (and below: RG3 .. RG10)
+#ifndef NMFC_BR_RGW
+#define NMFC_BR_RGW 0x21222334500ULL   // RG, W side: k = 2..10 -> 5 4 3 3 2 2 2 1 2
 #endif
-#ifndef NMFC_BR_RG3
-#define NMFC_BR_RG3 4
+#ifndef NMFC_BR_SPLH
+#define NMFC_BR_SPLH 0x300ULL          // bit k: 2 elements per lane (SPL), H side: k = 8, 9
 #endif
-#ifndef NMFC_BR_RG4
-#define NMFC_BR_RG4 5
+#ifndef NMFC_BR_SPLW
+#define NMFC_BR_SPLW 0x200ULL          // SPL, W side: k = 9
 #endif
-#ifndef NMFC_BR_RG5
-#define NMFC_BR_RG5 4
+#ifndef NMFC_BR_SLH
+#define NMFC_BR_SLH 0x6F0ULL           // bit k: operand rows by scalar loads (else LDS tiles), H side: k = 4..7, 9, 10
 #endif
-#ifndef NMFC_BR_RG6
-#define NMFC_BR_RG6 2
-#endif
-#ifndef NMFC_BR_RG7
-#define NMFC_BR_RG7 2
-#endif
-#ifndef NMFC_BR_RG10
-#define NMFC_BR_RG10 2
+#ifndef NMFC_BR_SLW
+#define NMFC_BR_SLW 0x7F0ULL           // scalar-load operand rows, W side: k = 4..10
 #endif
 #ifndef NMFC_BR_SMALL_B
 #define NMFC_BR_SMALL_B 32      // batches of at most this many restarts use rg_small
@@ -109,10 +106,9 @@
   ";NMFC_SMALL_PF=" NMFC_TUNING_STR(NMFC_SMALL_PF) ";NMFC_SMALL_FPF=" NMFC_TUNING_STR(NMFC_SMALL_FPF)                \
   ";NMFC_GT_PRIO=" NMFC_TUNING_STR(NMFC_GT_PRIO)
 #define NMFC_TUNING_BRUNET                                                                                           \
-  "NMFC_BRUNET_IEEEDIV=" NMFC_TUNING_STR(NMFC_BRUNET_IEEEDIV) ";NMFC_BR_SPL_MASK=" NMFC_TUNING_STR(NMFC_BR_SPL_MASK) \
-  ";NMFC_BR_RG2=" NMFC_TUNING_STR(NMFC_BR_RG2) ";NMFC_BR_RG3=" NMFC_TUNING_STR(NMFC_BR_RG3)                          \
-  ";NMFC_BR_RG4=" NMFC_TUNING_STR(NMFC_BR_RG4) ";NMFC_BR_RG5=" NMFC_TUNING_STR(NMFC_BR_RG5)                          \
-  ";NMFC_BR_RG6=" NMFC_TUNING_STR(NMFC_BR_RG6) ";NMFC_BR_RG7=" NMFC_TUNING_STR(NMFC_BR_RG7)                          \
-  ";NMFC_BR_RG10=" NMFC_TUNING_STR(NMFC_BR_RG10) ";NMFC_BR_SMALL_B=" NMFC_TUNING_STR(NMFC_BR_SMALL_B)                \
+  "NMFC_BRUNET_IEEEDIV=" NMFC_TUNING_STR(NMFC_BRUNET_IEEEDIV) ";NMFC_BR_RGH=" NMFC_TUNING_STR(NMFC_BR_RGH)           \
+  ";NMFC_BR_RGW=" NMFC_TUNING_STR(NMFC_BR_RGW) ";NMFC_BR_SPLH=" NMFC_TUNING_STR(NMFC_BR_SPLH)                        \
+  ";NMFC_BR_SPLW=" NMFC_TUNING_STR(NMFC_BR_SPLW) ";NMFC_BR_SLH=" NMFC_TUNING_STR(NMFC_BR_SLH)                        \
+  ";NMFC_BR_SLW=" NMFC_TUNING_STR(NMFC_BR_SLW) ";NMFC_BR_SMALL_B=" NMFC_TUNING_STR(NMFC_BR_SMALL_B)                  \
   ";NMFC_BR_RG_SMALL_DIV=" NMFC_TUNING_STR(NMFC_BR_RG_SMALL_DIV) ";NMFC_BR_TL=" NMFC_TUNING_STR(NMFC_BR_TL)          \
   ";NMFC_BR_UNROLL=" NMFC_TUNING_STR(NMFC_BR_UNROLL)
