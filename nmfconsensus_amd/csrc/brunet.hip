@@ -12,8 +12,9 @@
 // flop of rank-k products per restart with nothing to share but A: these are VALU kernels (fp64 FMA
 // + IEEE divide, the divide dominating for small k), not MFMA GEMMs.  A is shared by streaming one A
 // element per lane and applying it to RG restarts at once; the per-restart W row (H-side) or H column
-// (W-side) is wave-uniform and comes through scalar loads, so no LDS staging and no cross-lane
-// reductions are needed.  Layouts (per k batch of B restarts):
+// (W-side) is wave-uniform: it comes through scalar loads into SGPR operands, or for some ranks through
+// LDS tiles read back by broadcast (the per-k SL table below), and no cross-lane reductions are needed.
+// Layouts (per k batch of B restarts):
 //   Arm [m][n_pad] (sample-contiguous rows), Acm [n][m_pad] (gene-contiguous columns)
 //   W   [B][m][K]  (gene-major, k contiguous)    H [B][n][K]  (= libnmf column-major k x n)
 //   Gp  [chunk][B][K][n_pad]  split-K partials of W^T (A / VP) over fixed gene chunks
