@@ -205,13 +205,16 @@ __global__ __launch_bounds__(BT) void k_br_init(const uint32_t* __restrict__ see
 // HBM, fetched with coalesced vector loads one tile ahead into registers and stored into the other
 // half of a double-buffered LDS array; the inner loop reads it back with broadcast LDS reads.
 constexpr int TL = NMFC_BR_TL;
-// inner-loop unroll per k (measured, tools/brunet_kbench.py on the C5 shape: unroll 2 where the unrolled live ranges
-// push the register count past an occupancy step; round 5, with the one-step divide, re-measured against 2 / 4 / 8
-// for every k (profiles/r05/brunet/kbench_unroll_rg.txt): 8 for k = 4, 6 (-2.5 %, -10 % hnum + wupd), 2 for k = 8
-// (-12 %), k = 2, 3, 9 tied)
-constexpr int br_unroll(int K) {   // NMFC_BR_UNROLL != 0: one unroll for every k (experiment builds)
+// inner-loop unroll per k and kernel (tools/brunet_kbench.py on the C5 shape; unroll 2 where the unrolled live ranges
+// push the register count past an occupancy step).  Round 6, re-measured with the per-kernel SL / RG / SPL tables
+// against 1 / 2 / 4 / 8 for every k (profiles/r06/brunet_sload/n_*): H side 2 at k = 4 (-5 %), 4 at k = 6 (-8 %), 8 at
+// k = 10 (-6.5 %); W side 4 at k = 4 (-4 %), 2 at k = 6; the rest as round 5 (profiles/r05/brunet/kbench_unroll_rg.txt).
+constexpr int br_unroll_h(int K) {   // NMFC_BR_UNROLL != 0: one unroll for every k and kernel (experiment builds)
   return NMFC_BR_UNROLL != 0 ? NMFC_BR_UNROLL
-                             : (K == 4 || K == 6) ? 8 : (K == 5 || K == 7 || K == 8 || K == 10) ? 2 : 4;
+                             : K == 10 ? 8 : (K == 4 || K == 5 || K == 7 || K == 8) ? 2 : 4;
+}
+constexpr int br_unroll_w(int K) {
+  return NMFC_BR_UNROLL != 0 ? NMFC_BR_UNROLL : (K == 5 || K == 6 || K == 7 || K == 8 || K == 10) ? 2 : 4;
 }
 
 template <int K, int RG>
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
       }
     };
     if (i1 - t0 >= TL) {
-#pragma unroll br_unroll(K)
+#pragma unroll br_unroll_h(K)
       for (int ii = 0; ii < TL; ++ii) gene(ii);
     } else {
       for (int ii = 0; ii < i1 - t0; ++ii) gene(ii);
@@ -517,7 +520,7 @@ __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, 
       }
     };
     if (n - s0 >= TL) {
-#pragma unroll br_unroll(K)
+#pragma unroll br_unroll_w(K)
       for (int jj = 0; jj < TL; ++jj) sample(jj);
     } else {
       for (int jj = 0; jj < n - s0; ++jj) sample(jj);

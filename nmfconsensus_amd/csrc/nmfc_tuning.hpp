@@ -90,7 +90,7 @@
 #define NMFC_BR_TL 64           // operand tile rows
 #endif
 #ifndef NMFC_BR_UNROLL
-#define NMFC_BR_UNROLL 0        // 0: the measured per-k inner-loop unroll table (brunet.hip br_unroll)
+#define NMFC_BR_UNROLL 0        // 0: the measured per-k, per-kernel unroll tables (brunet.hip br_unroll_h / _w)
 #endif
 
 #define NMFC_TUNING_STR_(x) #x
