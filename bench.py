@@ -34,7 +34,8 @@ FP64_VALU_PEAK_TOPS = FP64_MFMA_PEAK_TFLOPS / 2
 # Brunet: VALU lane-instructions per matrix element and iteration, per side (H update, W update), as compiled
 # (csrc/brunet.hip, tools ISA listing): k FMAs of VP = W H, the divide q = a / VP (v_rcp_f64 + one Newton step
 # (2 FMA) + mul + residual FMA + correction FMA = 6; 8 with the second Newton step of rounds 1-4), k FMAs
-# accumulating W^T Q or Q H^T
+# accumulating W^T Q or Q H^T.  Round 6: N quotients share one v_rcp_f64 (batch inversion: N - 1 prefix multiplies, the
+# rcp and its Newton step, 2 (N - 1) back-multiplies = 3 N instructions for N reciprocals), still 6 per quotient
 BRUNET_DIV_OPS = 6
 # restart groups for the whole job on one GPU (the default C3 line): the fastest measured policy (with
 # the stream-K W^T A tile one group is fastest -- 500.7 vs 475.5 restarts/s for three, whose persistent launches queue behind
@@ -901,9 +902,11 @@ def bench_brunet(args, rank, world, local, dev):
                 "sweep_tflops": sweep_flop / (elapsed / args.steps) / 1e12,
                 "valu_ops_per_element_iteration": {str(k): brunet_valu_ops_per_element(k) for k in ks},
                 "note": "fp64 VALU issue roofline: per matrix element and iteration 2 x (2k FMA + the compiled divide, "
-                        f"{BRUNET_DIV_OPS} VALU instructions: rcp + 1 Newton step + mul + residual + correction), peak "
+                        f"{BRUNET_DIV_OPS} VALU instructions: the reciprocal (rcp + 1 Newton step, or its share of a batch "
+                        "inversion: 3 per quotient either way) + mul + residual + correction), peak "
                         "= 1024 SIMDs x 2.4 GHz x 16 fp64 lanes per cycle = 39.3 T lane-instructions/s (the 78.6 TF "
-                        "fp64 vector spec / 2); v_rcp_f64 is counted as one slot and address arithmetic not at all, so "
+                        "fp64 vector spec / 2); v_rcp_f64 (about 3 FMA issue slots, tools/quot_probe.hip rate mode) is "
+                        "counted as one slot and address arithmetic not at all, so "
                         "the fraction is a lower bound on VALU issue use; kernel rates from a serialized 40-iteration "
                         "pass per k (R restarts); rank_k_tflops counts the 8 m n k product flops alone"}
     cpu = None

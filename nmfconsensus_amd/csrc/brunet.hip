@@ -124,26 +124,61 @@ struct PinBuf {
   }
 };
 
-// q = a / p: rcp + one Newton step + one residual correction (Markstein's final step), i.e. the
-// compiler's IEEE sequence without its operand-scaling steps (div_scale / div_fmas / div_fixup), which
-// only matter near the exponent limits, and without its second Newton step.  v_rcp_f64 is good to
-// 2^-24.4 on gfx950, so one step leaves the reciprocal at ~2^-48.8 and the residual correction's error
-// at ~2^-97 relative before its rounding: the result is FAITHFUL, and it matched the correctly rounded a / p
-// on every one of 3.2e9 random probe pairs (tools/quot_probe.hip, a, p over 2^-60..2^10) -- but it is not
-// proven correctly rounded: a quotient can sit closer to a rounding midpoint (down to ~2^-106) than the
-// remaining error, and random pairs almost never hit those cases, so bit parity with an IEEE divide is
-// unpinned for them.  Here a >= 0 and p is a positive rank-k product of [eps, O(1)]-scaled factors; parity to
-// the IEEE-divide oracle on the tested sweeps: tests/test_gpu_brunet.py.  NMFC_BRUNET_IEEEDIV (a build of
-// tools/build_variant.sh) is the exact IEEE option.
-__device__ __forceinline__ double quot(double a, double p) {
+// q = a / p from a refined reciprocal r of p: q = a r and one residual correction (Markstein's final step), i.e. the
+// compiler's IEEE sequence without its operand-scaling steps (div_scale / div_fmas / div_fixup), which only matter
+// near the exponent limits, and without its second Newton step.  r comes from v_rcp_f64 (good to 2^-24.4 on gfx950)
+// and one Newton step (~2^-48.8), so the corrected quotient's error is ~2^-97 relative before its rounding: the result
+// is FAITHFUL, and it matched the correctly rounded a / p on every one of 3.2e9 random probe pairs (tools/quot_probe.hip,
+// a, p over 2^-60..2^10) -- but it is not proven correctly rounded: a quotient can sit closer to a rounding midpoint
+// (down to ~2^-106) than the remaining error, and random pairs almost never hit those cases, so bit parity with an IEEE
+// divide is unpinned for them.  Parity to the IEEE-divide oracle on the tested sweeps: tests/test_gpu_brunet.py.
+// NMFC_BRUNET_IEEEDIV (a build of tools/build_variant.sh) is the exact IEEE option.
+__device__ __forceinline__ double quot_r(double a, double p, double r) {
 #if NMFC_BRUNET_IEEEDIV
+  (void)r;
   return a / p;
 #else
-  double r = __builtin_amdgcn_rcp(p);
-  r = fma(r, fma(-p, r, 1.0), r);
   const double q = a * r;
   return fma(fma(-p, q, a), r, q);
 #endif
+}
+
+// Refined reciprocals of N positive values from ONE v_rcp_f64 (Montgomery's batch inversion): prefix products
+// c_i = p_0 ... p_i, u = 1 / c_{N-1} by v_rcp_f64 and one Newton step, then r_i = u c_{i-1} and u <- u p_i from the top
+// down (N = 1: v_rcp_f64 + one Newton step, the round-5 sequence).  v_rcp_f64 issues at about a third of the fp64 FMA
+// rate on gfx950 (6.9 vs 2.1 ns per wave instruction per SIMD, tools/quot_probe.hip rate mode,
+// profiles/r06/brunet_rcp/), so a batch of N trades N - 1 of them for 3 (N - 1) multiplies.  Each r_i carries the
+// Newton error plus at most 2 N roundings of 2^-53, so the corrected quotient keeps its ~2^-96 error and stays faithful
+// (0 differences from IEEE a / p in 3.2e9 batched probe quotients).  The prefix products must stay normal: with A
+// finite, non-negative and at most 2^64 (checked by nmfc_brunet_create) and caller factors in [2^-60, 2^60] (checked by
+// nmfc_brunet_run), every VP of the KL updates lies in [eps^2 / T, T] for T = sum(A) <= 2^100 -- the H update makes the
+// column sums of W H equal those of A (the W update the row sums), and the eps terms floor W and H at eps over the
+// row / column sums whose products are bounded by T -- so a batch of at most BR_RCP_MAX = 5
+// values spans at most 2^(5 (104 + 100)) = 2^1020.
+constexpr int BR_RCP_MAX = 5;
+template <int N>
+__device__ __forceinline__ void recip_batch(const double* p, double* r) {
+  static_assert(N >= 1 && N <= BR_RCP_MAX, "batch of 1 .. BR_RCP_MAX reciprocals");
+  double c[N];
+  c[0] = p[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) c[i] = c[i - 1] * p[i];
+  double u = __builtin_amdgcn_rcp(c[N - 1]);
+  u = fma(u, fma(-c[N - 1], u, 1.0), u);
+#pragma unroll
+  for (int i = N - 1; i > 0; --i) {
+    r[i] = u * c[i - 1];
+    u = u * p[i];
+  }
+  r[0] = u;
+}
+
+// reciprocals of NQ values in consecutive batches of at most B
+template <int NQ, int B>
+__device__ __forceinline__ void recips(const double* p, double* r) {
+  constexpr int N = NQ < B ? NQ : B;
+  recip_batch<N>(p, r);
+  if constexpr (NQ > N) recips<NQ - N, B>(p + N, r + N);
 }
 
 // Per-rank configuration of the two VALU kernels (tables in nmfc_tuning.hpp, per kernel since round 6):
@@ -156,6 +191,8 @@ __device__ __forceinline__ double quot(double a, double p) {
 //  SL   the wave-uniform operand rows by scalar loads into SGPR operands instead of the double-buffered LDS tiles: no
 //       LDS return-path bytes and no barriers, and the rows leave the VGPRs (occupancy up a step for k >= 4); the same
 //       arithmetic in the same order, so the same bits.
+//  RCP  the RG * SPL quotients of a lane's gene (sample) step take their reciprocals in batches of at most RCP from one
+//       v_rcp_f64 each (recip_batch); 1: one v_rcp_f64 per quotient.
 constexpr int br_nib(unsigned long long t, int K) { return K < 16 ? (int)((t >> (4 * K)) & 15) : 0; }
 constexpr int rgh_of(int K) { return br_nib(NMFC_BR_RGH, K) ? br_nib(NMFC_BR_RGH, K) : 1; }
 constexpr int rgw_of(int K) { return br_nib(NMFC_BR_RGW, K) ? br_nib(NMFC_BR_RGW, K) : 1; }
@@ -163,6 +200,9 @@ constexpr int splh_of(int K) { return ((NMFC_BR_SPLH >> K) & 1ULL) ? 2 : 1; }
 constexpr int splw_of(int K) { return ((NMFC_BR_SPLW >> K) & 1ULL) ? 2 : 1; }
 constexpr bool slh_of(int K) { return (NMFC_BR_SLH >> K) & 1ULL; }
 constexpr bool slw_of(int K) { return (NMFC_BR_SLW >> K) & 1ULL; }
+constexpr int rcp_clamp(int b) { return b < 1 ? 1 : (b > BR_RCP_MAX ? BR_RCP_MAX : b); }
+constexpr int rcph_of(int K) { return rcp_clamp(br_nib(NMFC_BR_RCPH, K)); }
+constexpr int rcpw_of(int K) { return rcp_clamp(br_nib(NMFC_BR_RCPW, K)); }
 // small batches (B <= NMFC_BR_SMALL_B restarts of one k, e.g. one rank's shard of a strong-scaling
 // run): fewer restarts per workgroup so the batch still spreads over the CUs
 constexpr int rg_small(int rg) {
@@ -295,27 +335,36 @@ __global__ __launch_bounds__(BT) void k_br_hnum(const double* __restrict__ Arm, 
     const double* ap = Arm + (long)t0 * n_pad;
     const double* wt = wl[buf];
     const double* wg = W + (long)t0 * K;
-    // slots past the live restarts repeat the last live one (computed, never stored): no branches here
+    // one gene: every quotient's VP first, their reciprocals in batches of rcph_of(K) (recips), then the accumulations
+    // (each accumulator still adds its genes in gene order).  Slots past the live restarts repeat the last live one
+    // (computed, never stored): no branches here
     auto gene = [&](int ii) {
-      double a[SPL];
+      constexpr int NQ = RG * SPL;
+      double a[SPL], w[RG][K], p[NQ], rr[NQ];
 #pragma unroll
       for (int s = 0; s < SPL; ++s) a[s] = ap[(long)ii * n_pad + jl[s]];
 #pragma unroll
       for (int r = 0; r < RG; ++r) {
         const double* wr = SL ? wg + wro[r] + ii * K : wt + r * (TL * K) + ii * K;
-        double w[K];
 #pragma unroll
-        for (int c = 0; c < K; ++c) w[c] = wr[c];
+        for (int c = 0; c < K; ++c) w[r][c] = wr[c];
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
-          double p = 0.0;
+          double v = 0.0;
 #pragma unroll
-          for (int c = 0; c < K; ++c) p = fma(w[c], h[s][r][c], p);
-          const double q = quot(a[s], p);
-#pragma unroll
-          for (int c = 0; c < K; ++c) g[s][r][c] = fma(w[c], q, g[s][r][c]);
+          for (int c = 0; c < K; ++c) v = fma(w[r][c], h[s][r][c], v);
+          p[r * SPL + s] = v;
         }
       }
+      recips<NQ, rcph_of(K)>(p, rr);
+#pragma unroll
+      for (int r = 0; r < RG; ++r)
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+          const double q = quot_r(a[s], p[r * SPL + s], rr[r * SPL + s]);
+#pragma unroll
+          for (int c = 0; c < K; ++c) g[s][r][c] = fma(w[r][c], q, g[s][r][c]);
+        }
     };
     if (i1 - t0 >= TL) {
 #pragma unroll br_unroll_h(K)
@@ -498,26 +547,34 @@ __global__ __launch_bounds__(BT) void k_br_wupd(const double* __restrict__ Acm, 
     const double* ap = Acm + (long)s0 * m_pad;
     const double* ht = hl[buf];
     const double* hg = H + (long)s0 * K;
+    // one sample, as the H side's gene(): VPs, batched reciprocals, accumulations
     auto sample = [&](int jj) {
-      double a[SPL];
+      constexpr int NQ = RG * SPL;
+      double a[SPL], hh[RG][K], p[NQ], rr[NQ];
 #pragma unroll
       for (int s = 0; s < SPL; ++s) a[s] = ap[(long)jj * m_pad + il[s]];
 #pragma unroll
       for (int r = 0; r < RG; ++r) {
         const double* hj = SL ? hg + hro[r] + jj * K : ht + r * (TL * K) + jj * K;
-        double hh[K];
 #pragma unroll
-        for (int c = 0; c < K; ++c) hh[c] = hj[c];
+        for (int c = 0; c < K; ++c) hh[r][c] = hj[c];
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
-          double p = 0.0;
+          double v = 0.0;
 #pragma unroll
-          for (int c = 0; c < K; ++c) p = fma(w[s][r][c], hh[c], p);
-          const double q = quot(a[s], p);
-#pragma unroll
-          for (int c = 0; c < K; ++c) f[s][r][c] = fma(q, hh[c], f[s][r][c]);
+          for (int c = 0; c < K; ++c) v = fma(w[s][r][c], hh[r][c], v);
+          p[r * SPL + s] = v;
         }
       }
+      recips<NQ, rcpw_of(K)>(p, rr);
+#pragma unroll
+      for (int r = 0; r < RG; ++r)
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+          const double q = quot_r(a[s], p[r * SPL + s], rr[r * SPL + s]);
+#pragma unroll
+          for (int c = 0; c < K; ++c) f[s][r][c] = fma(q, hh[r][c], f[s][r][c]);
+        }
     };
     if (n - s0 >= TL) {
 #pragma unroll br_unroll_w(K)
@@ -572,13 +629,16 @@ __global__ void k_br_divide(const int32_t* __restrict__ counts, double denom, lo
   if (i < len) out[i] = (double)counts[i] / denom;
 }
 
+// ... and the domain check of recip_batch: *bad = 1 (a plain store; every writer stores the same value) when an entry
+// is not a finite number in [0, 2^64]
 __global__ void k_br_layout(const double* __restrict__ A, int m, int n, long m_pad, long n_pad,
-                            double* __restrict__ Acm, double* __restrict__ Arm) {
+                            double* __restrict__ Acm, double* __restrict__ Arm, int* __restrict__ bad) {
   const int i = blockIdx.x * BT + threadIdx.x, j = blockIdx.y;
   if (i >= m) return;
   const double v = A[(long)j * m + i];
   Acm[(long)j * m_pad + i] = v;
   Arm[(long)i * n_pad + j] = v;
+  if (!(v >= 0.0 && v <= 0x1p64)) *bad = 1;   // NaN fails both tests
 }
 
 }  // namespace
@@ -792,7 +852,16 @@ int br_run_k(nmfc_brunet* e, BrLane* L, const KJob& kj, int B, int R, const nmfc
   for (int b = 0; b < B; ++b) seeds[b] = o.seed + (uint32_t)(rb + b + 1);   // set.seed(rseed + i), i 1-based
   BCHECK(hipMemcpyAsync(L->seeds.p, seeds, sizeof(uint32_t) * B, hipMemcpyHostToDevice, st));
   if (W_init && H_init) {
-    // caller factors for this k's B jobs: W_b m x K column-major, H_b K x n column-major
+    // caller factors for this k's B jobs: W_b m x K column-major, H_b K x n column-major; positive and within
+    // [2^-60, 2^60] (the batched reciprocals' domain, recip_batch)
+    const size_t nwk = (size_t)B * m * K, nhk = (size_t)B * n * K;
+    for (size_t x = 0; x < nwk + nhk; ++x) {
+      const double v = x < nwk ? W_init[kj.woff + x] : H_init[kj.hoff + (x - nwk)];
+      if (!(v >= 0x1p-60 && v <= 0x1p60)) {
+        br_err("nmfc_brunet_run: caller factors must lie in [2^-60, 2^60] (k=%d: %g)", K, v);
+        return -1;
+      }
+    }
     hw.assign((size_t)B * m * K, 0.0);
     for (int b = 0; b < B; ++b)
       for (int c = 0; c < K; ++c)
@@ -899,11 +968,27 @@ nmfc_brunet* nmfc_brunet_create(int device, const double* A, int m, int n, int a
       return fail("upload A", err);
     dA = tmp.as<double>();
   }
+  Buf dbad;
+  if (dbad.ensure(sizeof(int))) {
+    nmfc_brunet_destroy(e);
+    return nullptr;
+  }
+  if ((err = hipMemsetAsync(dbad.p, 0, sizeof(int), e->st)) != hipSuccess) return fail("memset", err);
   hipLaunchKernelGGL(k_br_layout, dim3((m + BT - 1) / BT, n), dim3(BT), 0, e->st, dA, m, n, e->m_pad, e->n_pad,
-                     e->Acm.as<double>(), e->Arm.as<double>());
+                     e->Acm.as<double>(), e->Arm.as<double>(), dbad.as<int>());
   if ((err = hipGetLastError()) != hipSuccess) return fail("k_br_layout", err);
+  int bad = 0;
+  if ((err = hipMemcpyAsync(&bad, dbad.p, sizeof(int), hipMemcpyDeviceToHost, e->st)) != hipSuccess)
+    return fail("read-back", err);
   if ((err = hipStreamSynchronize(e->st)) != hipSuccess) return fail("sync", err);
   tmp.release();
+  dbad.release();
+  if (bad) {
+    // the KL updates need A >= 0; the bound keeps the batched reciprocals' products normal (recip_batch)
+    br_err("nmfc_brunet_create: A must hold finite, non-negative entries of at most 2^64");
+    nmfc_brunet_destroy(e);
+    return nullptr;
+  }
   return e;
 }
 

@@ -92,6 +92,12 @@
 #ifndef NMFC_BR_UNROLL
 #define NMFC_BR_UNROLL 0        // 0: the measured per-k, per-kernel unroll tables (brunet.hip br_unroll_h / _w)
 #endif
+#ifndef NMFC_BR_RCPH
+#define NMFC_BR_RCPH 0x12221222200ULL  // nibble k: quotients sharing one v_rcp_f64 (brunet.hip recip_batch), H side: k = 2..10 -> 2 2 2 2 1 2 2 2 1
+#endif
+#ifndef NMFC_BR_RCPW
+#define NMFC_BR_RCPW 0x22222242500ULL  // the same, W side: k = 2..10 -> 5 2 4 2 2 2 2 2 2
+#endif
 
 #define NMFC_TUNING_STR_(x) #x
 #define NMFC_TUNING_STR(x) NMFC_TUNING_STR_(x)
@@ -111,4 +117,5 @@
   ";NMFC_BR_SPLW=" NMFC_TUNING_STR(NMFC_BR_SPLW) ";NMFC_BR_SLH=" NMFC_TUNING_STR(NMFC_BR_SLH)                        \
   ";NMFC_BR_SLW=" NMFC_TUNING_STR(NMFC_BR_SLW) ";NMFC_BR_SMALL_B=" NMFC_TUNING_STR(NMFC_BR_SMALL_B)                  \
   ";NMFC_BR_RG_SMALL_DIV=" NMFC_TUNING_STR(NMFC_BR_RG_SMALL_DIV) ";NMFC_BR_TL=" NMFC_TUNING_STR(NMFC_BR_TL)          \
-  ";NMFC_BR_UNROLL=" NMFC_TUNING_STR(NMFC_BR_UNROLL)
+  ";NMFC_BR_UNROLL=" NMFC_TUNING_STR(NMFC_BR_UNROLL) ";NMFC_BR_RCPH=" NMFC_TUNING_STR(NMFC_BR_RCPH)              \
+  ";NMFC_BR_RCPW=" NMFC_TUNING_STR(NMFC_BR_RCPW)

@@ -148,6 +148,17 @@ def test_bad_arguments():
             eng.run([17], 1)
         with pytest.raises(RuntimeError):
             eng.run([2], 1, stopfreq=0)
+        # caller factors outside [2^-60, 2^60] (the batched reciprocals' domain, brunet.hip recip_batch)
+        W0, H0 = np.full((10, 2), 0.5), np.full((2, 4), 0.5)
+        W0[3, 1] = 0.0
+        with pytest.raises(RuntimeError, match="caller factors"):
+            eng.run([2], 1, maxiter=2, W_init=[W0], H_init=[H0])
+    # A: finite, non-negative, at most 2^64
+    for bad in (-1.0, np.nan, np.inf, 1e30):
+        B = np.ones((10, 4))
+        B[7, 2] = bad
+        with pytest.raises(RuntimeError, match="non-negative"):
+            BrunetEngine(B)
 
 
 def test_c5_full_size_stop_rule_vs_oracle():

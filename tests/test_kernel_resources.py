@@ -90,12 +90,22 @@ def test_no_register_spills():
 def test_brunet_divide_op_count_matches_isa():
     """bench.py's C5 roofline prices each quotient at BRUNET_DIV_OPS fp64 VALU instructions beside the 2k rank-k FMAs
     (ADVICE r04): the innermost loop of k_br_hnum / k_br_wupd must hold exactly 2k + BRUNET_DIV_OPS fp64 VALU
-    instructions per quotient (one v_rcp_f64 each), so the figure cannot drift from the compiled code."""
+    instructions per quotient, so the figure cannot drift from the compiled code.  Round 6: the RG x SPL quotients of a
+    gene (sample) step share v_rcp_f64s in batches of the kernel's RCP table entry (brunet.hip recip_batch: 3 fp64
+    instructions per quotient for the reciprocal either way), so a loop holds ceil(RG SPL / RCP) v_rcp_f64 per
+    RG SPL quotients."""
+    import re
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from bench import BRUNET_DIV_OPS
     import isa_loop
+
+    defaults = _tuning_defaults()
+
+    def rcp_batch(side, k):
+        v = (int(defaults["NMFC_BR_RCP" + side].rstrip("ULul"), 0) >> (4 * k)) & 15
+        return min(max(v, 1), 5)
 
     with tempfile.TemporaryDirectory() as td:
         s = os.path.join(td, "b.s")
@@ -104,16 +114,20 @@ def test_brunet_divide_op_count_matches_isa():
         assert r.returncode == 0, r.stderr[-2000:]
         lines = open(s).read().splitlines()
     # scalar-load operand rows (k = 10, 5) and the LDS-tile form (k = 2, 3)
-    for kern, k in (("k_br_hnumILi10ELi1ELi1ELb1E", 10), ("k_br_wupdILi10ELi2ELi1ELb1E", 10),
-                    ("k_br_hnumILi5ELi3ELi1ELb1E", 5), ("k_br_wupdILi5ELi3ELi1ELb1E", 5),
-                    ("k_br_hnumILi2ELi5ELi1ELb0E", 2), ("k_br_wupdILi3ELi4ELi1ELb0E", 3)):
+    for kern in ("k_br_hnumILi10ELi1ELi1ELb1E", "k_br_wupdILi10ELi2ELi1ELb1E", "k_br_hnumILi5ELi3ELi1ELb1E",
+                 "k_br_wupdILi5ELi3ELi1ELb1E", "k_br_hnumILi2ELi5ELi1ELb0E", "k_br_wupdILi3ELi4ELi1ELb0E"):
+        k, rg, spl = (int(x) for x in re.findall(r"ILi(\d+)ELi(\d+)ELi(\d+)E", kern)[0])
+        nq = rg * spl
+        b = rcp_batch("H" if "hnum" in kern else "W", k)
+        rcps_per_step = -(-nq // b)
         body = isa_loop.kernel_body(lines, kern)
         inner = isa_loop.innermost_loop_with(body, "v_rcp_f64")
         ops = [x.split()[0] for x in inner]
         n_rcp = sum(1 for o in ops if o.startswith("v_rcp_f64"))
         n_f64 = sum(1 for o in ops if o.startswith("v_") and "f64" in o and not o.startswith("v_mfma"))
-        assert n_rcp > 0, kern
-        assert n_f64 == n_rcp * (2 * k + BRUNET_DIV_OPS), (kern, n_f64, n_rcp)
+        assert n_rcp > 0 and n_rcp % rcps_per_step == 0, (kern, n_rcp, rcps_per_step)
+        n_quot = n_rcp // rcps_per_step * nq
+        assert n_f64 == n_quot * (2 * k + BRUNET_DIV_OPS), (kern, n_f64, n_rcp, n_quot)
 
 
 def _tuning_defaults():
