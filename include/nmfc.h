@@ -169,10 +169,13 @@ typedef struct nmfc_brunet_opts {
 typedef struct nmfc_brunet nmfc_brunet;
 
 void nmfc_brunet_default_opts(nmfc_brunet_opts* o);
+/* A: m x n column-major, every entry finite, >= 0 and <= 2^64 (else NULL with nmfc_last_error set): the domain in
+ * which the kernels' batched reciprocals stay normal (csrc/brunet.hip recip_batch). */
 nmfc_brunet* nmfc_brunet_create(int device, const double* A, int m, int n, int a_on_device);
 void nmfc_brunet_destroy(nmfc_brunet* e);
 int nmfc_brunet_device(const nmfc_brunet* e);   /* as nmfc_engine_device */
-/* W_init/H_init (optional, host): every job of the shard in output order. Returns 0 or -1 (nmfc_last_error). */
+/* W_init/H_init (optional, host): every job of the shard in output order, entries in [2^-60, 2^60].
+ * Returns 0 or -1 (nmfc_last_error). */
 int nmfc_brunet_run(nmfc_brunet* e, const int* ks, int nk, int R, const nmfc_brunet_opts* opts, const double* W_init,
                     const double* H_init, nmfc_result* out);
 void nmfc_brunet_set_timing(nmfc_brunet* e, int enable);
